@@ -1,0 +1,221 @@
+"""bench.py -- RandBLAS sketch-apply on MI355X: sketched entries/s and fraction of roofline.
+
+Workload (BASELINE.json configs[1], the metric's single-GPU config): Gaussian skge, fp64,
+B (d x n) = S (d x m) * A (m x n) with S ~ DenseDist(d, m) (key 0, MajorAxis::Long) regenerated
+inside the fused MFMA GEMM, A ~ DenseDist(m, n) Gaussian key 99 ColMajor (generated on the device,
+resident in HBM before timing), d = 1024, m = n = 16384, alpha = 1, beta = 0.
+
+A "step" is one sketch_general call over the whole A. With N > 1 ranks (torchrun, RCCL) the job is
+weak-scaled by output rows: rank g computes rows [g*d, (g+1)*d) of the (N*d) x n sketch of the
+operator DenseDist(N*d, m) (ro_s = g*d, the reference's reproducible-submatrix property) and an
+RCCL all-gather reassembles the full ColMajor sketch on every rank inside the timed step.
+
+Prints ONE JSON line (rank 0). value = N*d*n / t_step (entries/s, whole job); roofline = the fused
+GEMM kernel's algorithmic flops (2*d*m*n per launch) / its average launch time measured with HIP
+events on the launch stream; cpu_baseline = the oracle's OpenMP fill + host BLAS dgemm (the
+reference's algorithm, oracle/) on a bounded column sample, rank 0 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import randblas_amd as rb  # noqa: E402
+
+PEAK = {"f64": 78.6e12, "f32": 157.3e12}   # MI355X dense matrix peaks (MI355X_MICROARCH.md)
+HBM_PEAK = 8.0e12
+
+CONFIGS = {
+    # name: (kind, dtype, d, m, n, vec_nnz)
+    "c2": ("dense", "f64", 1024, 16384, 16384, 0),
+    "ns": ("dense", "f64", 2048, 16384, 16384, 0),
+    "c3": ("saso", "f64", 1024, 16384, 16384, 8),
+    "c4": ("dense", "f32", 2048, 32768, 32768, 0),
+    "c5": ("sksy", "f64", 512, 16384, 16384, 0),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(kind, dtype, d, m, n, vec_nnz, target_s=10.0):
+    """The oracle (reference algorithm restated in C + host BLAS) on a bounded sample of columns."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+
+    cores = os.cpu_count() or 1
+    O.set_threads(cores)
+    npdt = np.float64 if dtype == "f64" else np.float32
+
+    def run(ns):
+        A, _ = O.fill_dense("C", m, ns, "G", "L", m, ns, 0, 0, key=99, dtype=npdt)
+        B = np.zeros(d * ns, dtype=npdt)
+        t0 = time.perf_counter()
+        if kind == "saso":
+            rows, cols, vals = O.fill_sparse(d, m, vec_nnz, "S", key=0, dtype=npdt)
+            O.left_spmm_coo("C", "N", "N", d, ns, m, 1.0, d, m, rows, cols, vals, 0, 0, A, m, 0.0, B, d)
+        else:
+            O.lskge3("C", "N", "N", d, ns, m, 1.0, d, m, "G", "L", 0, 0, 0, A, m, 0.0, B, d)
+        return time.perf_counter() - t0
+
+    ns = 64
+    t = run(ns)   # warm-up + calibration
+    while t < 0.5 and ns < n:
+        ns = min(n, ns * 4)
+        t = run(ns)
+    reps = max(1, min(5, int(target_s / max(t, 1e-3))))
+    times = [run(ns) for _ in range(reps)]
+    tmed = float(np.median(times))
+    return {
+        "value": d * ns / tmed,
+        "unit": "sketched entries/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": f"{kind} {dtype} d={d} m={m} on {ns} of the {n} columns of A, median of {reps} "
+                  f"(OpenMP Philox/Box-Muller fill + {os.path.basename(O.BLAS)} gemm)" if kind != "saso" else
+                  f"saso {dtype} d={d} m={m} vec_nnz={vec_nnz} on {ns} of {n} columns, median of {reps}",
+        "seconds": tmed,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    kind, dtype, d, m, n, vec_nnz = CONFIGS[args.config]
+    tdt = torch.float64 if dtype == "f64" else torch.float32
+    stream = torch.cuda.current_stream(dev)
+
+    # A ~ DenseDist(m, n) Gaussian key 99, ColMajor, generated on the device (input, not timed)
+    A = torch.empty(m * n, dtype=tdt, device=dev)
+    rb.fill_dense("C", rb.DenseDist(m, n), m, n, 0, 0, A, rb.RNGState(99))
+    B = torch.empty(d * n, dtype=tdt, device=dev)
+    full = torch.empty(world * d * n, dtype=tdt, device=dev) if world > 1 else None
+    gathered = torch.empty(world * d * n, dtype=tdt, device=dev) if world > 1 else None
+    if kind == "saso":
+        S = rb.SparseSkOp(rb.SparseDist(world * d, m, vec_nnz), rb.RNGState(0))
+    else:
+        S = rb.DenseSkOp(rb.DenseDist(world * d, m), rb.RNGState(0))
+    if kind == "sksy":   # A symmetric: A := (A + A^T) / 2 (input prep, not timed)
+        Am = A.view(n, m)
+        A.copy_(((Am + Am.t()) * 0.5).reshape(-1))
+
+    k_ev = []
+
+    def step(record=False):
+        e0 = e1 = None
+        if record:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        if kind == "sksy":
+            rb.sketch_symmetric_left("C", d, n, 1.0, S, A, m, 0.0, B, d, ro_s=rank * d, sym_check_tol=-1.0)
+        else:
+            rb.sketch_general_left("C", "N", "N", d, n, m, 1.0, S, A, m, 0.0, B, d, ro_s=rank * d)
+        if record:
+            e1.record(stream)
+            k_ev.append((e0, e1))
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, B)
+            # [world][n][d] (each shard ColMajor d x n) -> ColMajor (world*d) x n
+            full.view(n, world * d).copy_(gathered.view(world, n, d).permute(1, 0, 2).reshape(n, world * d))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(record=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in k_ev]))
+    ms_step = elapsed * 1e3 / args.steps
+
+    # roofline of the dominant kernel
+    if kind == "saso":
+        alg = m * n * (8 if dtype == "f64" else 4) + d * n * (8 if dtype == "f64" else 4)
+        achieved = alg / (kern_ms * 1e-3)
+        roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK, "traffic": None}
+    else:
+        flops = 2.0 * d * m * n
+        achieved = flops / (kern_ms * 1e-3)
+        roof = {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK[dtype] / 1e12, "unit": "TFLOP/s",
+                "frac": achieved / PEAK[dtype], "traffic": None}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(kind, dtype, d, m, n, vec_nnz)
+        except Exception as e:  # the baseline never blocks the GPU line
+            log(f"cpu_baseline failed: {e!r}")
+
+    if rank == 0:
+        line = {
+            "metric": "sketched-entries/sec (d*n/s) + achieved-%-of-fp64-MFMA-peak, skge d x m * m x n",
+            "value": world * d * n / (ms_step * 1e-3),
+            "unit": "sketched entries/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "kernel_ms": kern_ms,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": dtype,
+            "data": "synthetic (A ~ Gaussian DenseDist(m,n) key 99 generated on device; S regenerated in-kernel)",
+            "config": {"workload": {"c2": "Gaussian skge fp64 (BASELINE configs[1])",
+                                    "ns": "Gaussian skge fp64 north-star",
+                                    "c3": "SASO SparseSkOp vec_nnz=8 fp64 (configs[2])",
+                                    "c4": "Gaussian skge fp32 (configs[3])",
+                                    "c5": "sksy fp64 (configs[4])"}[args.config],
+                       "d": world * d, "d_per_gpu": d, "m": m, "n": n, "layout": "ColMajor",
+                       "operator": "SparseSkOp SASO" if kind == "saso" else "DenseSkOp Gaussian MajorAxis::Long",
+                       "parallelism": f"row-shard x{world} + RCCL all-gather" if world > 1 else "single GPU"},
+            "pct_of_peak": roof["frac"] * 100.0,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,147 @@
+/* randblas_hip.h -- C ABI of librandblas_hip.so, the MI355X (gfx950) implementation of RandBLAS's
+ * sketch-apply path.
+ *
+ * Reference: RylieWeaver/RandBLAS snapshot 2024-10-08, a header-only C++20 library whose extension
+ * model is vendor re-implementation of its API (README.md:6-7). Each entry point below replaces
+ * one function of that API; the file:line it replaces is given with it. The C++ drop-in header
+ * include/RandBLAS.hh wraps these entry points in the reference's own types and overloads.
+ *
+ * Conventions
+ *   layout: 'C' = blas::Layout::ColMajor, 'R' = RowMajor.   op: 'N' = NoTrans, 'T' = Trans.
+ *   family: 'G' Gaussian, 'U' Uniform, 'B' BlackBox (DenseDistName, dense_skops.hh:204-218).
+ *   major_axis: 'L' Long, 'S' Short, 'U' Undefined (MajorAxis, base.hh:138-150).
+ *   Matrix pointers may be device memory (hipMalloc / torch tensors) or host memory. Host
+ *   arrays are staged through device memory and the call is synchronous (the reference's
+ *   semantics); with device arrays the work is enqueued on `stream` (NULL = default stream) and
+ *   the call returns without synchronising.
+ *   Every function returns RBH_OK (0) or an error code; rbh_last_error() gives the message of the
+ *   last failure on the calling thread, in the reference's randblas_require format
+ *   ("(cond) was required, but did not hold, in function f", exceptions.hh:135-161).
+ */
+#ifndef RANDBLAS_HIP_H
+#define RANDBLAS_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RBH_OK 0
+#define RBH_ERR_REQUIRE 1   /* a randblas_require() of the reference would have thrown */
+#define RBH_ERR_HIP 2       /* HIP runtime / launch failure */
+#define RBH_ERR_SYMMETRY 3  /* util::require_symmetric failed (util.hh:165-188) */
+
+/* RNGState<r123::Philox4x32> (base.hh:161-232): 128-bit counter (little-endian u32 words) + key. */
+typedef struct rbh_state {
+    uint32_t counter[4];
+    uint32_t key[2];
+} rbh_state;
+
+/* DenseDist (dense_skops.hh:222-294). */
+typedef struct rbh_dense_dist {
+    int64_t n_rows;
+    int64_t n_cols;
+    char family;
+    char major_axis;
+} rbh_dense_dist;
+
+/* SparseDist (sparse_skops.hh:134-165). */
+typedef struct rbh_sparse_dist {
+    int64_t n_rows;
+    int64_t n_cols;
+    int64_t vec_nnz;
+    char major_axis;
+} rbh_sparse_dist;
+
+int rbh_abi_version(void);
+const char *rbh_last_error(void);
+
+/* ---- RNG state bookkeeping --------------------------------------------------------------- */
+/* dense::compute_next_state (dense_skops.hh:172-191). */
+int rbh_dense_next_state(const rbh_dense_dist *D, const rbh_state *seed, rbh_state *next);
+/* sparse::compute_next_state (sparse_skops.hh:115-126), quirk kept. */
+int rbh_sparse_next_state(const rbh_sparse_dist *D, const rbh_state *seed, rbh_state *next);
+/* Number of nonzeros a SparseSkOp of D holds (sparse_skops.hh:351-360). */
+int64_t rbh_sparse_nnz(const rbh_sparse_dist *D);
+
+/* ---- samplers -------------------------------------------------------------------------- */
+/* RandBLAS::fill_dense(layout, D, n_rows, n_cols, ro_s, co_s, buff, seed) (dense_skops.hh:486-532).
+ * next_state may be NULL; it receives the state fill_dense returns. */
+int rbh_fill_dense_f64(char layout, const rbh_dense_dist *D, int64_t n_rows, int64_t n_cols, int64_t ro_s,
+                       int64_t co_s, double *buff, const rbh_state *seed, rbh_state *next_state, void *stream);
+int rbh_fill_dense_f32(char layout, const rbh_dense_dist *D, int64_t n_rows, int64_t n_cols, int64_t ro_s,
+                       int64_t co_s, float *buff, const rbh_state *seed, rbh_state *next_state, void *stream);
+
+/* RandBLAS::fill_sparse(S) (sparse_skops.hh:389-413): writes rbh_sparse_nnz(D) COO entries in the
+ * reference's order (per minor-axis vector, Fisher-Yates draw order). vals may be NULL. */
+int rbh_fill_sparse_f64(const rbh_sparse_dist *D, const rbh_state *seed, int64_t *rows, int64_t *cols,
+                        double *vals, void *stream);
+int rbh_fill_sparse_f32(const rbh_sparse_dist *D, const rbh_state *seed, int64_t *rows, int64_t *cols,
+                        float *vals, void *stream);
+
+/* ---- sketch_general, dense operator ------------------------------------------------------ */
+/* Left: B = alpha * op(submat(S)) * op(A) + beta * B, B is d x n, op(submat(S)) is d x m at
+ * (ro_s, co_s) of S ~ D.  Replaces sketch_general(layout, opS, opA, d, n, m, alpha, DenseSkOp& S,
+ * ro_s, co_s, A, lda, beta, B, ldb) (skge.hh:814-836 -> dense::lskge3, skge.hh:173-215).
+ * S_buff == NULL: the operator is regenerated inside the GEMM from (D, seed) and never stored
+ * (the fused path). S_buff != NULL: S is the dense D.n_rows x D.n_cols matrix in S_layout (a
+ * user-filled DenseSkOp::buff or a BlackBox operator, dense_skops.hh:215-217, 410-411). */
+int rbh_lskge3_f64(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, double alpha,
+                   const rbh_dense_dist *D, const rbh_state *seed, const double *S_buff, char S_layout,
+                   int64_t ro_s, int64_t co_s, const double *A, int64_t lda, double beta, double *B, int64_t ldb,
+                   void *stream);
+int rbh_lskge3_f32(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, float alpha,
+                   const rbh_dense_dist *D, const rbh_state *seed, const float *S_buff, char S_layout,
+                   int64_t ro_s, int64_t co_s, const float *A, int64_t lda, float beta, float *B, int64_t ldb,
+                   void *stream);
+/* Right: B = alpha * op(A) * op(submat(S)) + beta * B, B is m x d, op(submat(S)) is n x d.
+ * Replaces sketch_general(layout, opA, opS, m, d, n, alpha, A, lda, DenseSkOp& S, ro_s, co_s,
+ * beta, B, ldb) (skge.hh:943-1007 -> dense::rskge3, skge.hh:320-364). */
+int rbh_rskge3_f64(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, double alpha,
+                   const double *A, int64_t lda, const rbh_dense_dist *D, const rbh_state *seed,
+                   const double *S_buff, char S_layout, int64_t ro_s, int64_t co_s, double beta, double *B,
+                   int64_t ldb, void *stream);
+int rbh_rskge3_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, float alpha,
+                   const float *A, int64_t lda, const rbh_dense_dist *D, const rbh_state *seed,
+                   const float *S_buff, char S_layout, int64_t ro_s, int64_t co_s, float beta, float *B,
+                   int64_t ldb, void *stream);
+
+/* ---- sketch_general, sparse operator ----------------------------------------------------- */
+/* Left: B = alpha * op(submat(S)) * op(A) + beta * B with S a SparseSkOp of D.
+ * Replaces sketch_general(..., SparseSkOp& S, ...) (skge.hh:790-812 -> sparse::lskges,
+ * skge.hh:485-510 -> left_spmm, sparse_data/spmm_dispatch.hh:48-160 -> apply_coo_left_jki_p11,
+ * coo_spmm_impl.hh:79-162). rows == NULL: the operator is sampled on the device from (D, seed)
+ * (fill_sparse); otherwise (rows, cols, vals) hold nnz COO entries (any order). Each entry of B
+ * is accumulated in ascending order of the contracted index with separate multiply and add, as
+ * apply_csc_to_vector_from_left_ki (csc_spmm_impl.hh:43-65) does, so results are bitwise those
+ * of the reference's scalar loop. */
+int rbh_lskges_f64(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, double alpha,
+                   const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz, const int64_t *rows,
+                   const int64_t *cols, const double *vals, int64_t ro_s, int64_t co_s, const double *A,
+                   int64_t lda, double beta, double *B, int64_t ldb, void *stream);
+int rbh_lskges_f32(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, float alpha,
+                   const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz, const int64_t *rows,
+                   const int64_t *cols, const float *vals, int64_t ro_s, int64_t co_s, const float *A,
+                   int64_t lda, float beta, float *B, int64_t ldb, void *stream);
+/* Right: B = alpha * op(A) * op(submat(S)) + beta * B (skge.hh:616-641 -> right_spmm,
+ * spmm_dispatch.hh:162-200). */
+int rbh_rskges_f64(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, double alpha,
+                   const double *A, int64_t lda, const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz,
+                   const int64_t *rows, const int64_t *cols, const double *vals, int64_t ro_s, int64_t co_s,
+                   double beta, double *B, int64_t ldb, void *stream);
+int rbh_rskges_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, float alpha,
+                   const float *A, int64_t lda, const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz,
+                   const int64_t *rows, const int64_t *cols, const float *vals, int64_t ro_s, int64_t co_s,
+                   float beta, float *B, int64_t ldb, void *stream);
+
+/* ---- sketch_symmetric support ------------------------------------------------------------- */
+/* util::require_symmetric (util.hh:165-188) on the device: RBH_OK if |A_ij - A_ji| <=
+ * (|A_ij| + |A_ji| + 1) * tol for all i < j (tol < 0 skips the check), else RBH_ERR_SYMMETRY.
+ * sketch_symmetric (sksy.hh:165-537) = this check + the sketch_general entry points above. */
+int rbh_require_symmetric_f64(char layout, const double *A, int64_t n, int64_t lda, double tol, void *stream);
+int rbh_require_symmetric_f32(char layout, const float *A, int64_t n, int64_t lda, float tol, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RANDBLAS_HIP_H */

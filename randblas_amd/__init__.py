@@ -1,0 +1,349 @@
+"""randblas_amd -- MI355X (gfx950) implementation of RandBLAS's sketch-apply path.
+
+The product is the C-ABI library ``librandblas_hip.so`` (declared in ``include/randblas_hip.h``);
+C++ callers use the drop-in header ``include/RandBLAS.hh``. This module is the thin Python
+binding used by the tests and ``bench.py``: it mirrors the reference's operator API
+(``RNGState``, ``DenseDist``, ``DenseSkOp``, ``SparseDist``, ``SparseSkOp``, ``sketch_general``,
+``sketch_symmetric``, ``fill_dense``, ``fill_sparse``; RandBLAS/skge.hh:771-1214,
+RandBLAS/sksy.hh:165-537, RandBLAS/dense_skops.hh:486-592, RandBLAS/sparse_skops.hh:389-413)
+and passes torch device tensors (or host numpy arrays) straight through to the C ABI.
+
+There is no CPU fallback: if the HIP library is missing, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librandblas_hip.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"randblas_amd: {LIB_PATH} is missing; build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+    )
+lib = ctypes.CDLL(LIB_PATH)
+
+c_i64 = ctypes.c_int64
+c_char = ctypes.c_char
+c_vp = ctypes.c_void_p
+
+RBH_OK, RBH_ERR_REQUIRE, RBH_ERR_HIP, RBH_ERR_SYMMETRY = 0, 1, 2, 3
+
+
+class RNGStateC(ctypes.Structure):
+    _fields_ = [("counter", ctypes.c_uint32 * 4), ("key", ctypes.c_uint32 * 2)]
+
+
+class DenseDistC(ctypes.Structure):
+    _fields_ = [("n_rows", c_i64), ("n_cols", c_i64), ("family", c_char), ("major_axis", c_char)]
+
+
+class SparseDistC(ctypes.Structure):
+    _fields_ = [("n_rows", c_i64), ("n_cols", c_i64), ("vec_nnz", c_i64), ("major_axis", c_char)]
+
+
+class RandBLASError(RuntimeError):
+    """RandBLAS::exceptions::Error equivalent (RandBLAS/exceptions.hh:45-70)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+
+
+def _check(rc: int) -> None:
+    if rc != RBH_OK:
+        raise RandBLASError(rc, lib.rbh_last_error().decode())
+
+
+# --------------------------------------------------------------------------------------------
+# signatures
+# --------------------------------------------------------------------------------------------
+P = ctypes.POINTER
+lib.rbh_last_error.restype = ctypes.c_char_p
+lib.rbh_abi_version.restype = ctypes.c_int
+lib.rbh_sparse_nnz.restype = c_i64
+lib.rbh_sparse_nnz.argtypes = [P(SparseDistC)]
+lib.rbh_dense_next_state.argtypes = [P(DenseDistC), P(RNGStateC), P(RNGStateC)]
+lib.rbh_sparse_next_state.argtypes = [P(SparseDistC), P(RNGStateC), P(RNGStateC)]
+for _t, _ct in (("f64", ctypes.c_double), ("f32", ctypes.c_float)):
+    getattr(lib, f"rbh_fill_dense_{_t}").argtypes = [c_char, P(DenseDistC), c_i64, c_i64, c_i64, c_i64, c_vp,
+                                                     P(RNGStateC), P(RNGStateC), c_vp]
+    getattr(lib, f"rbh_fill_sparse_{_t}").argtypes = [P(SparseDistC), P(RNGStateC), c_vp, c_vp, c_vp, c_vp]
+    getattr(lib, f"rbh_lskge3_{_t}").argtypes = [c_char, c_char, c_char, c_i64, c_i64, c_i64, _ct, P(DenseDistC),
+                                                 P(RNGStateC), c_vp, c_char, c_i64, c_i64, c_vp, c_i64, _ct, c_vp,
+                                                 c_i64, c_vp]
+    getattr(lib, f"rbh_rskge3_{_t}").argtypes = [c_char, c_char, c_char, c_i64, c_i64, c_i64, _ct, c_vp, c_i64,
+                                                 P(DenseDistC), P(RNGStateC), c_vp, c_char, c_i64, c_i64, _ct, c_vp,
+                                                 c_i64, c_vp]
+    getattr(lib, f"rbh_lskges_{_t}").argtypes = [c_char, c_char, c_char, c_i64, c_i64, c_i64, _ct, P(SparseDistC),
+                                                 P(RNGStateC), c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64,
+                                                 _ct, c_vp, c_i64, c_vp]
+    getattr(lib, f"rbh_rskges_{_t}").argtypes = [c_char, c_char, c_char, c_i64, c_i64, c_i64, _ct, c_vp, c_i64,
+                                                 P(SparseDistC), P(RNGStateC), c_i64, c_vp, c_vp, c_vp, c_i64, c_i64,
+                                                 _ct, c_vp, c_i64, c_vp]
+    getattr(lib, f"rbh_require_symmetric_{_t}").argtypes = [c_char, c_vp, c_i64, c_i64, _ct, c_vp]
+
+# --------------------------------------------------------------------------------------------
+# Python mirror of the reference's types
+# --------------------------------------------------------------------------------------------
+Layout_ColMajor, Layout_RowMajor = "C", "R"
+Op_NoTrans, Op_Trans = "N", "T"
+
+
+@dataclass
+class RNGState:
+    """RNGState<r123::Philox4x32> (RandBLAS/base.hh:161-232). RNGState(k): counter 0, key {k, 0}."""
+
+    key: int = 0
+    counter: tuple = (0, 0, 0, 0)
+    key_hi: int = 0
+
+    def c(self) -> RNGStateC:
+        s = RNGStateC()
+        for i in range(4):
+            s.counter[i] = int(self.counter[i]) & 0xFFFFFFFF
+        s.key[0] = int(self.key) & 0xFFFFFFFF
+        s.key[1] = int(self.key_hi) & 0xFFFFFFFF
+        return s
+
+    @staticmethod
+    def from_c(s: RNGStateC) -> "RNGState":
+        return RNGState(key=s.key[0], counter=tuple(s.counter), key_hi=s.key[1])
+
+
+@dataclass
+class DenseDist:
+    """DenseDist (RandBLAS/dense_skops.hh:222-294); family 'G'/'U'/'B', major_axis 'L'/'S'/'U'."""
+
+    n_rows: int
+    n_cols: int
+    family: str = "G"
+    major_axis: Optional[str] = None
+
+    def __post_init__(self):
+        if self.major_axis is None:
+            self.major_axis = "U" if self.family == "B" else "L"
+
+    def c(self) -> DenseDistC:
+        return DenseDistC(self.n_rows, self.n_cols, self.family.encode(), self.major_axis.encode())
+
+
+@dataclass
+class SparseDist:
+    """SparseDist (RandBLAS/sparse_skops.hh:134-165); major_axis 'S' (SASO) or 'L' (LASO)."""
+
+    n_rows: int
+    n_cols: int
+    vec_nnz: int
+    major_axis: str = "S"
+
+    def c(self) -> SparseDistC:
+        return SparseDistC(self.n_rows, self.n_cols, self.vec_nnz, self.major_axis.encode())
+
+    @property
+    def nnz(self) -> int:
+        return int(lib.rbh_sparse_nnz(ctypes.byref(self.c())))
+
+
+def dense_next_state(D: DenseDist, seed: RNGState) -> RNGState:
+    out = RNGStateC()
+    _check(lib.rbh_dense_next_state(ctypes.byref(D.c()), ctypes.byref(seed.c()), ctypes.byref(out)))
+    return RNGState.from_c(out)
+
+
+def sparse_next_state(D: SparseDist, seed: RNGState) -> RNGState:
+    out = RNGStateC()
+    _check(lib.rbh_sparse_next_state(ctypes.byref(D.c()), ctypes.byref(seed.c()), ctypes.byref(out)))
+    return RNGState.from_c(out)
+
+
+@dataclass
+class DenseSkOp:
+    """DenseSkOp<T> (RandBLAS/dense_skops.hh:332-419). buff None = lazy (the fused path regenerates
+    the operator inside the GEMM); a buff (device tensor / host array) with buff_layout makes it
+    an explicit operator (user-filled or BlackBox)."""
+
+    dist: DenseDist
+    seed_state: RNGState
+    buff: object = None
+    buff_layout: str = "C"
+
+    @property
+    def n_rows(self):
+        return self.dist.n_rows
+
+    @property
+    def n_cols(self):
+        return self.dist.n_cols
+
+    @property
+    def next_state(self) -> RNGState:
+        return dense_next_state(self.dist, self.seed_state)
+
+
+@dataclass
+class SparseSkOp:
+    """SparseSkOp<T> (RandBLAS/sparse_skops.hh:183-377). rows/cols/vals None = sample on the device at
+    apply time (fill_sparse); otherwise the COO arrays (device or host) define the operator."""
+
+    dist: SparseDist
+    seed_state: RNGState
+    rows: object = None
+    cols: object = None
+    vals: object = None
+    nnz: Optional[int] = None
+
+    @property
+    def n_rows(self):
+        return self.dist.n_rows
+
+    @property
+    def n_cols(self):
+        return self.dist.n_cols
+
+    @property
+    def next_state(self) -> RNGState:
+        return sparse_next_state(self.dist, self.seed_state)
+
+
+# --------------------------------------------------------------------------------------------
+# helpers
+# --------------------------------------------------------------------------------------------
+def _ptr(x):
+    if x is None:
+        return None
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    raise TypeError(f"unsupported array type {type(x)}")
+
+
+def _dtype_tag(x) -> str:
+    dt = str(x.dtype)
+    if dt in ("float64", "torch.float64"):
+        return "f64"
+    if dt in ("float32", "torch.float32"):
+        return "f32"
+    raise TypeError(f"unsupported dtype {dt}")
+
+
+def _stream(x, stream):
+    if stream is not None:
+        return stream
+    try:
+        import torch
+
+        if isinstance(x, torch.Tensor) and x.is_cuda:
+            return torch.cuda.current_stream(x.device).cuda_stream
+    except ImportError:  # pragma: no cover
+        pass
+    return None
+
+
+def _b(s: str) -> bytes:
+    return s.encode()
+
+
+# --------------------------------------------------------------------------------------------
+# API
+# --------------------------------------------------------------------------------------------
+def fill_dense(layout, D: DenseDist, n_rows, n_cols, ro_s, co_s, buff, seed: RNGState, stream=None) -> RNGState:
+    """RandBLAS::fill_dense(layout, D, n_rows, n_cols, ro_s, co_s, buff, seed) (dense_skops.hh:486-532)."""
+    t = _dtype_tag(buff)
+    nxt = RNGStateC()
+    fn = getattr(lib, f"rbh_fill_dense_{t}")
+    _check(fn(_b(layout), ctypes.byref(D.c()), n_rows, n_cols, ro_s, co_s, _ptr(buff), ctypes.byref(seed.c()),
+              ctypes.byref(nxt), _stream(buff, stream)))
+    return RNGState.from_c(nxt)
+
+
+def fill_sparse(S: SparseSkOp, rows, cols, vals, stream=None) -> None:
+    """RandBLAS::fill_sparse(S) (sparse_skops.hh:389-413) into the given COO arrays."""
+    t = _dtype_tag(vals)
+    fn = getattr(lib, f"rbh_fill_sparse_{t}")
+    _check(fn(ctypes.byref(S.dist.c()), ctypes.byref(S.seed_state.c()), _ptr(rows), _ptr(cols), _ptr(vals),
+              _stream(vals, stream)))
+
+
+def sketch_general_left(layout, opS, opA, d, n, m, alpha, S, A, lda, beta, B, ldb, ro_s=0, co_s=0, stream=None):
+    """B = alpha op(submat(S)) op(A) + beta B (RandBLAS::sketch_general, skge.hh:771-836, 1088-1112)."""
+    t = _dtype_tag(B)
+    st = _stream(B, stream)
+    if isinstance(S, DenseSkOp):
+        fn = getattr(lib, f"rbh_lskge3_{t}")
+        _check(fn(_b(layout), _b(opS), _b(opA), d, n, m, alpha, ctypes.byref(S.dist.c()),
+                  ctypes.byref(S.seed_state.c()), _ptr(S.buff), _b(S.buff_layout), ro_s, co_s, _ptr(A), lda, beta,
+                  _ptr(B), ldb, st))
+    elif isinstance(S, SparseSkOp):
+        fn = getattr(lib, f"rbh_lskges_{t}")
+        nnz = S.nnz if S.nnz is not None else (S.dist.nnz if S.rows is not None else 0)
+        _check(fn(_b(layout), _b(opS), _b(opA), d, n, m, alpha, ctypes.byref(S.dist.c()),
+                  ctypes.byref(S.seed_state.c()), nnz, _ptr(S.rows), _ptr(S.cols), _ptr(S.vals), ro_s, co_s, _ptr(A),
+                  lda, beta, _ptr(B), ldb, st))
+    else:
+        raise TypeError("S must be a DenseSkOp or SparseSkOp")
+
+
+def sketch_general_right(layout, opA, opS, m, d, n, alpha, A, lda, S, beta, B, ldb, ro_s=0, co_s=0, stream=None):
+    """B = alpha op(A) op(submat(S)) + beta B (RandBLAS::sketch_general, skge.hh:943-1007, 1190-1214)."""
+    t = _dtype_tag(B)
+    st = _stream(B, stream)
+    if isinstance(S, DenseSkOp):
+        fn = getattr(lib, f"rbh_rskge3_{t}")
+        _check(fn(_b(layout), _b(opA), _b(opS), m, d, n, alpha, _ptr(A), lda, ctypes.byref(S.dist.c()),
+                  ctypes.byref(S.seed_state.c()), _ptr(S.buff), _b(S.buff_layout), ro_s, co_s, beta, _ptr(B), ldb,
+                  st))
+    elif isinstance(S, SparseSkOp):
+        fn = getattr(lib, f"rbh_rskges_{t}")
+        nnz = S.nnz if S.nnz is not None else (S.dist.nnz if S.rows is not None else 0)
+        _check(fn(_b(layout), _b(opA), _b(opS), m, d, n, alpha, _ptr(A), lda, ctypes.byref(S.dist.c()),
+                  ctypes.byref(S.seed_state.c()), nnz, _ptr(S.rows), _ptr(S.cols), _ptr(S.vals), ro_s, co_s, beta,
+                  _ptr(B), ldb, st))
+    else:
+        raise TypeError("S must be a DenseSkOp or SparseSkOp")
+
+
+def require_symmetric(layout, A, n, lda, tol, stream=None) -> None:
+    """util::require_symmetric (RandBLAS/util.hh:165-188) on the device."""
+    t = _dtype_tag(A)
+    fn = getattr(lib, f"rbh_require_symmetric_{t}")
+    _check(fn(_b(layout), _ptr(A), n, lda, tol, _stream(A, stream)))
+
+
+def sketch_symmetric_left(layout, d, n, alpha, S, A, lda, beta, B, ldb, ro_s=0, co_s=0, sym_check_tol=0.0,
+                          stream=None):
+    """B = alpha S A + beta B, A symmetric n x n in general storage (sksy.hh:300-319 / 520-537)."""
+    require_symmetric(layout, A, n, lda, sym_check_tol, stream)
+    sketch_general_left(layout, "N", "N", d, n, n, alpha, S, A, lda, beta, B, ldb, ro_s, co_s, stream)
+
+
+def sketch_symmetric_right(layout, n, d, alpha, A, lda, S, beta, B, ldb, ro_s=0, co_s=0, sym_check_tol=0.0,
+                           stream=None):
+    """B = alpha A S + beta B, A symmetric n x n in general storage (sksy.hh:165-184 / 413-430)."""
+    require_symmetric(layout, A, n, lda, sym_check_tol, stream)
+    sketch_general_right(layout, "N", "N", n, d, n, alpha, A, lda, S, beta, B, ldb, ro_s, co_s, stream)
+
+
+def sketch_general(layout, op1, op2, d_or_m, n_or_d, m_or_n, alpha, X, Y, lda_or_none, *args, **kw):
+    """Overload dispatcher mirroring RandBLAS::sketch_general: left form when X is an operator."""
+    if isinstance(X, (DenseSkOp, SparseSkOp)):
+        return sketch_general_left(layout, op1, op2, d_or_m, n_or_d, m_or_n, alpha, X, Y, lda_or_none, *args, **kw)
+    return sketch_general_right(layout, op1, op2, d_or_m, n_or_d, m_or_n, alpha, X, Y, lda_or_none, *args, **kw)
+
+
+def abi_version() -> int:
+    return int(lib.rbh_abi_version())
+
+
+__all__ = [
+    "RNGState", "DenseDist", "SparseDist", "DenseSkOp", "SparseSkOp", "RandBLASError", "fill_dense", "fill_sparse",
+    "sketch_general", "sketch_general_left", "sketch_general_right", "sketch_symmetric_left",
+    "sketch_symmetric_right", "require_symmetric", "dense_next_state", "sparse_next_state", "abi_version", "lib",
+    "LIB_PATH",
+]

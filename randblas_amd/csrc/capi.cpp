@@ -1,0 +1,730 @@
+// capi.cpp -- the C ABI of librandblas_hip.so (include/randblas_hip.h).
+//
+// Argument checking follows the reference's randblas_require calls (same conditions, same message
+// format); then every {left, right} x {ColMajor, RowMajor} x {opS, opA} x {dense, sparse} case is
+// reduced to one canonical device problem:
+//   dense : C[M x N] (col-major) = alpha X[M x K] Y[K x N] + beta C      (skge_dense.hip)
+//   sparse: C(i,j) = beta C(i,j) + sum_k asc (alpha S'(i,k)) Y(k,j)      (saso.hip)
+// Host (non-device) arrays are staged through device memory so the reference's host-pointer API
+// works unchanged; device arrays are used in place and the work is stream-ordered.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/randblas_hip.h"
+#include "common.hpp"
+#include "saso.hpp"
+
+using namespace rbh;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int set_error(int code, const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define RBH_REQUIRE(cond)                                                                                  \
+    do {                                                                                                   \
+        if (!(cond))                                                                                       \
+            return set_error(RBH_ERR_REQUIRE, "(%s) was required, but did not hold, in function %s", #cond, \
+                             __func__);                                                                    \
+    } while (0)
+
+#define RBH_HIP(expr)                                                                                 \
+    do {                                                                                              \
+        hipError_t e_ = (expr);                                                                       \
+        if (e_ != hipSuccess) return set_error(RBH_ERR_HIP, "HIP error %s (%d) at %s:%d: %s",          \
+                                               hipGetErrorName(e_), (int)e_, __FILE__, __LINE__, #expr); \
+    } while (0)
+
+bool is_device_ptr(const void *p) {
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    hipError_t e = hipPointerGetAttributes(&a, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+// Number of elements a rows x cols matrix with leading dimension ld spans in layout.
+int64_t extent(char layout, int64_t rows, int64_t cols, int64_t ld) {
+    if (rows <= 0 || cols <= 0) return 0;
+    return layout == 'C' ? ld * (cols - 1) + rows : ld * (rows - 1) + cols;
+}
+
+// A host or device buffer seen from the device. Host buffers get a device copy (in: copied
+// H2D; out: copied back D2H by finish()).
+struct Staged {
+    void *host = nullptr;
+    void *dev = nullptr;
+    size_t bytes = 0;
+    bool owned = false;
+    bool out = false;
+};
+
+struct Stager {
+    hipStream_t s;
+    std::vector<Staged> v;
+    bool any_host = false;
+    explicit Stager(hipStream_t st) : s(st) {}
+    // returns device pointer (or nullptr on error / null input)
+    hipError_t map(const void *p, size_t bytes, bool copy_in, bool out, void **dptr) {
+        *dptr = nullptr;
+        if (!p || bytes == 0) { *dptr = const_cast<void *>(p); return hipSuccess; }
+        if (is_device_ptr(p)) { *dptr = const_cast<void *>(p); return hipSuccess; }
+        any_host = true;
+        Staged st;
+        st.host = const_cast<void *>(p);
+        st.bytes = bytes;
+        st.out = out;
+        st.owned = true;
+        hipError_t e = hipMalloc(&st.dev, bytes);
+        if (e != hipSuccess) return e;
+        if (copy_in) {
+            e = hipMemcpyAsync(st.dev, p, bytes, hipMemcpyHostToDevice, s);
+            if (e != hipSuccess) { (void)hipFree(st.dev); return e; }
+        }
+        v.push_back(st);
+        *dptr = st.dev;
+        return hipSuccess;
+    }
+    hipError_t finish() {
+        hipError_t err = hipSuccess;
+        for (auto &st : v)
+            if (st.out) {
+                hipError_t e = hipMemcpyAsync(st.host, st.dev, st.bytes, hipMemcpyDeviceToHost, s);
+                if (e != hipSuccess && err == hipSuccess) err = e;
+            }
+        if (any_host) {
+            hipError_t e = hipStreamSynchronize(s);
+            if (e != hipSuccess && err == hipSuccess) err = e;
+        }
+        for (auto &st : v)
+            if (st.owned) (void)hipFree(st.dev);
+        v.clear();
+        return err;
+    }
+    ~Stager() {
+        for (auto &st : v)
+            if (st.owned) (void)hipFree(st.dev);
+    }
+};
+
+char dist_to_layout(const rbh_dense_dist *D) {   // dense_skops.hh:297-310
+    const bool is_wide = D->n_rows < D->n_cols;
+    const bool fa_long = D->major_axis == 'L';
+    if (is_wide && fa_long) return 'R';
+    if (is_wide) return 'C';
+    if (fa_long) return 'C';
+    return 'R';
+}
+
+int64_t major_axis_length(const rbh_dense_dist *D) {   // dense_skops.hh:312-316
+    return D->major_axis == 'L' ? std::max(D->n_rows, D->n_cols) : std::min(D->n_rows, D->n_cols);
+}
+
+template <typename T>
+void make_gen(GenOperand &g, const rbh_dense_dist *D, const rbh_state *seed, int64_t ro, int64_t co,
+              bool o_is_window_row, int &kind) {
+    const bool nat_row = dist_to_layout(D) == 'R';
+    const int64_t L = major_axis_length(D);
+    memcpy(g.ctr, seed->counter, sizeof g.ctr);
+    memcpy(g.key, seed->key, sizeof g.key);
+    g.stride = (uint64_t)((L + 3) / 4);
+    g.pr0 = nat_row ? ro : co;
+    g.pc0 = nat_row ? co : ro;
+    g.family = D->family == 'U' ? rb::UNIFORM : rb::GAUSSIAN;
+    g.scale = (double)(T)std::sqrt(3.0);
+    kind = (o_is_window_row == nat_row) ? GEN_OK : GEN_OO;
+}
+
+template <typename T>
+int mem_mode(const void *ptr, int64_t so, int64_t sk, int64_t K) {
+    const int vec = 16 / (int)sizeof(T);
+    if (sk != 1) return 0;
+    if (((uintptr_t)ptr % 16) == 0 && ((so * (int64_t)sizeof(T)) % 16) == 0 && (K % vec) == 0) return 2;
+    return 1;
+}
+
+template <typename T> hipError_t launch_gemm_t(const GemmProblem &p, hipStream_t s);
+template <> hipError_t launch_gemm_t<double>(const GemmProblem &p, hipStream_t s) { return launch_gemm_f64(p, s); }
+template <> hipError_t launch_gemm_t<float>(const GemmProblem &p, hipStream_t s) { return launch_gemm_f32(p, s); }
+template <typename T> hipError_t launch_scale_t(int64_t M, int64_t N, T b, T *C, int64_t ldc, hipStream_t s);
+template <> hipError_t launch_scale_t<double>(int64_t M, int64_t N, double b, double *C, int64_t ldc, hipStream_t s) {
+    return launch_scale_f64(M, N, b, C, ldc, s);
+}
+template <> hipError_t launch_scale_t<float>(int64_t M, int64_t N, float b, float *C, int64_t ldc, hipStream_t s) {
+    return launch_scale_f32(M, N, b, C, ldc, s);
+}
+
+// Canonical dense GEMM launch: X/Y either generated (S window) or memory.
+template <typename T>
+int run_dense(GemmProblem &p, hipStream_t s) {
+    if (p.M <= 0 || p.N <= 0) return RBH_OK;
+    if (p.K <= 0 || p.alpha == 0.0) {
+        RBH_HIP(launch_scale_t<T>(p.M, p.N, (T)p.beta, (T *)p.C, p.ldc, s));
+        return RBH_OK;
+    }
+    RBH_HIP(launch_gemm_t<T>(p, s));
+    return RBH_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// dense left: B = alpha op(submat(S)) op(A) + beta B        (dense::lskge3, skge.hh:173-215)
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+int lskge3(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, T alpha, const rbh_dense_dist *D,
+           const rbh_state *seed, const T *S_buff, char S_layout, int64_t ro_s, int64_t co_s, const T *A,
+           int64_t lda, T beta, T *B, int64_t ldb, void *stream) {
+    RBH_REQUIRE(layout == 'C' || layout == 'R');
+    RBH_REQUIRE(opS == 'N' || opS == 'T');
+    RBH_REQUIRE(opA == 'N' || opA == 'T');
+    RBH_REQUIRE(D != nullptr);
+    RBH_REQUIRE(d >= 0 && n >= 0 && m >= 0 && ro_s >= 0 && co_s >= 0);
+    const int64_t rows_submat_S = opS == 'N' ? d : m, cols_submat_S = opS == 'N' ? m : d;
+    RBH_REQUIRE(D->n_rows >= rows_submat_S + ro_s);
+    RBH_REQUIRE(D->n_cols >= cols_submat_S + co_s);
+    const int64_t rows_A = opA == 'N' ? m : n, cols_A = opA == 'N' ? n : m;
+    if (layout == 'C') {
+        RBH_REQUIRE(lda >= rows_A);
+        RBH_REQUIRE(ldb >= d);
+    } else {
+        RBH_REQUIRE(lda >= cols_A);
+        RBH_REQUIRE(ldb >= n);
+    }
+    if (!S_buff) {
+        RBH_REQUIRE(seed != nullptr);
+        RBH_REQUIRE(D->family != 'B');
+        RBH_REQUIRE(D->major_axis != 'U');
+    } else {
+        RBH_REQUIRE(S_layout == 'C' || S_layout == 'R');
+    }
+    hipStream_t s = (hipStream_t)stream;
+    Stager st(s);
+    void *dA, *dB, *dS;
+    RBH_HIP(st.map(A, sizeof(T) * extent(layout, rows_A, cols_A, lda), true, false, &dA));
+    RBH_HIP(st.map(B, sizeof(T) * extent(layout, d, n, ldb), beta != (T)0, true, &dB));
+    RBH_HIP(st.map(S_buff, sizeof(T) * D->n_rows * D->n_cols, true, false, &dS));
+
+    GemmProblem p{};
+    p.alpha = alpha;
+    p.beta = beta;
+    p.C = dB;
+    p.ldc = ldb;
+    const bool col = layout == 'C';
+    // op(submat(S)) as an operand whose outer index is the output row i of B: outer == window row iff opS == N
+    const bool s_outer_is_row = opS == 'N';
+    GenOperand sg{};
+    MemOperand sm{};
+    int skind = MEM;
+    if (!dS) {
+        make_gen<T>(sg, D, seed, ro_s, co_s, s_outer_is_row, skind);
+    } else {
+        const int64_t rs = S_layout == 'C' ? 1 : D->n_cols, cs = S_layout == 'C' ? D->n_rows : 1;
+        sm.ptr = (const T *)dS + ro_s * rs + co_s * cs;
+        sm.so = s_outer_is_row ? rs : cs;
+        sm.sk = s_outer_is_row ? cs : rs;
+    }
+    // op(A): element (k, j)
+    MemOperand am{};
+    am.ptr = dA;
+    if (col) { am.so = opA == 'N' ? lda : 1; am.sk = opA == 'N' ? 1 : lda; }
+    else { am.so = opA == 'N' ? 1 : lda; am.sk = opA == 'N' ? lda : 1; }
+    if (col) {   // C = B (d x n): X = op(submat S), Y = op(A)
+        p.M = d; p.N = n; p.K = m;
+        p.xkind = skind; p.xg = sg; p.xm = sm;
+        p.ykind = MEM; p.ym = am;
+    } else {     // C = B^T (n x d): X = op(A)^T, Y = op(submat S)^T
+        p.M = n; p.N = d; p.K = m;
+        p.xkind = MEM; p.xm = am;
+        p.ykind = skind; p.yg = sg; p.ym = sm;
+    }
+    p.xmode = p.xkind == MEM ? mem_mode<T>(p.xm.ptr, p.xm.so, p.xm.sk, p.K) : 0;
+    p.ymode = p.ykind == MEM ? mem_mode<T>(p.ym.ptr, p.ym.so, p.ym.sk, p.K) : 0;
+    int rc = run_dense<T>(p, s);
+    if (rc) return rc;
+    RBH_HIP(st.finish());
+    return RBH_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// dense right: B = alpha op(A) op(submat(S)) + beta B       (dense::rskge3, skge.hh:320-364)
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+int rskge3(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, T alpha, const T *A, int64_t lda,
+           const rbh_dense_dist *D, const rbh_state *seed, const T *S_buff, char S_layout, int64_t ro_s,
+           int64_t co_s, T beta, T *B, int64_t ldb, void *stream) {
+    RBH_REQUIRE(layout == 'C' || layout == 'R');
+    RBH_REQUIRE(opS == 'N' || opS == 'T');
+    RBH_REQUIRE(opA == 'N' || opA == 'T');
+    RBH_REQUIRE(D != nullptr);
+    RBH_REQUIRE(d >= 0 && n >= 0 && m >= 0 && ro_s >= 0 && co_s >= 0);
+    const int64_t rows_submat_S = opS == 'N' ? n : d, cols_submat_S = opS == 'N' ? d : n;
+    RBH_REQUIRE(D->n_rows >= rows_submat_S + ro_s);
+    RBH_REQUIRE(D->n_cols >= cols_submat_S + co_s);
+    const int64_t rows_A = opA == 'N' ? m : n, cols_A = opA == 'N' ? n : m;
+    if (layout == 'C') {
+        RBH_REQUIRE(lda >= rows_A);
+        RBH_REQUIRE(ldb >= m);
+    } else {
+        RBH_REQUIRE(lda >= cols_A);
+        RBH_REQUIRE(ldb >= d);
+    }
+    if (!S_buff) {
+        RBH_REQUIRE(seed != nullptr);
+        RBH_REQUIRE(D->family != 'B');
+        RBH_REQUIRE(D->major_axis != 'U');
+    } else {
+        RBH_REQUIRE(S_layout == 'C' || S_layout == 'R');
+    }
+    hipStream_t s = (hipStream_t)stream;
+    Stager st(s);
+    void *dA, *dB, *dS;
+    RBH_HIP(st.map(A, sizeof(T) * extent(layout, rows_A, cols_A, lda), true, false, &dA));
+    RBH_HIP(st.map(B, sizeof(T) * extent(layout, m, d, ldb), beta != (T)0, true, &dB));
+    RBH_HIP(st.map(S_buff, sizeof(T) * D->n_rows * D->n_cols, true, false, &dS));
+
+    GemmProblem p{};
+    p.alpha = alpha;
+    p.beta = beta;
+    p.C = dB;
+    p.ldc = ldb;
+    const bool col = layout == 'C';
+    // op(submat(S)) (n x d) as an operand whose outer index is its column j (0..d):
+    // outer == window row iff opS == T
+    const bool s_outer_is_row = opS == 'T';
+    GenOperand sg{};
+    MemOperand sm{};
+    int skind = MEM;
+    if (!dS) {
+        make_gen<T>(sg, D, seed, ro_s, co_s, s_outer_is_row, skind);
+    } else {
+        const int64_t rs = S_layout == 'C' ? 1 : D->n_cols, cs = S_layout == 'C' ? D->n_rows : 1;
+        sm.ptr = (const T *)dS + ro_s * rs + co_s * cs;
+        sm.so = s_outer_is_row ? rs : cs;
+        sm.sk = s_outer_is_row ? cs : rs;
+    }
+    // op(A) (m x n): element (i, k)
+    MemOperand am{};
+    am.ptr = dA;
+    if (col) { am.so = opA == 'N' ? 1 : lda; am.sk = opA == 'N' ? lda : 1; }
+    else { am.so = opA == 'N' ? lda : 1; am.sk = opA == 'N' ? 1 : lda; }
+    if (col) {   // C = B (m x d): X = op(A), Y = op(submat S)
+        p.M = m; p.N = d; p.K = n;
+        p.xkind = MEM; p.xm = am;
+        p.ykind = skind; p.yg = sg; p.ym = sm;
+    } else {     // C = B^T (d x m): X = op(submat S)^T, Y = op(A)^T
+        p.M = d; p.N = m; p.K = n;
+        p.xkind = skind; p.xg = sg; p.xm = sm;
+        p.ykind = MEM; p.ym = am;
+    }
+    p.xmode = p.xkind == MEM ? mem_mode<T>(p.xm.ptr, p.xm.so, p.xm.sk, p.K) : 0;
+    p.ymode = p.ykind == MEM ? mem_mode<T>(p.ym.ptr, p.ym.so, p.ym.sk, p.K) : 0;
+    int rc = run_dense<T>(p, s);
+    if (rc) return rc;
+    RBH_HIP(st.finish());
+    return RBH_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// fill_dense (dense_skops.hh:486-532)
+// ---------------------------------------------------------------------------------------------
+template <typename T> hipError_t launch_fill_t(const GenOperand &, int64_t, int64_t, int, T *, hipStream_t);
+template <> hipError_t launch_fill_t<double>(const GenOperand &g, int64_t r, int64_t c, int t, double *b, hipStream_t s) {
+    return launch_fill_dense_f64(g, r, c, t, b, s);
+}
+template <> hipError_t launch_fill_t<float>(const GenOperand &g, int64_t r, int64_t c, int t, float *b, hipStream_t s) {
+    return launch_fill_dense_f32(g, r, c, t, b, s);
+}
+
+void dense_next(const rbh_dense_dist *D, const rbh_state *seed, rbh_state *next) {   // dense_skops.hh:172-191
+    *next = *seed;
+    if (D->major_axis == 'U') return;
+    const int64_t major_len = major_axis_length(D);
+    const int64_t minor_len = D->n_rows + (D->n_cols - major_len);
+    const int64_t stride = (major_len + 3) / 4;
+    rb::ctr_add(seed->counter, (uint64_t)(stride * minor_len), next->counter);
+}
+
+template <typename T>
+int fill_dense(char layout, const rbh_dense_dist *D, int64_t n_rows, int64_t n_cols, int64_t ro_s, int64_t co_s,
+               T *buff, const rbh_state *seed, rbh_state *next_state, void *stream) {
+    RBH_REQUIRE(D != nullptr && seed != nullptr);
+    RBH_REQUIRE(layout == 'C' || layout == 'R');
+    RBH_REQUIRE(n_rows >= 0 && n_cols >= 0 && ro_s >= 0 && co_s >= 0);
+    RBH_REQUIRE(D->n_rows >= n_rows + ro_s);
+    RBH_REQUIRE(D->n_cols >= n_cols + co_s);
+    RBH_REQUIRE(D->family != 'B');
+    RBH_REQUIRE(D->major_axis != 'U');
+    const char nat = dist_to_layout(D);
+    const int64_t L = major_axis_length(D);
+    int64_t n_rows_, n_cols_;
+    GenOperand g{};
+    memcpy(g.ctr, seed->counter, sizeof g.ctr);
+    memcpy(g.key, seed->key, sizeof g.key);
+    g.stride = (uint64_t)((L + 3) / 4);
+    g.family = D->family == 'U' ? rb::UNIFORM : rb::GAUSSIAN;
+    g.scale = (double)(T)std::sqrt(3.0);
+    if (nat == 'C') { n_rows_ = n_cols; n_cols_ = n_rows; g.pr0 = co_s; g.pc0 = ro_s; }
+    else { n_rows_ = n_rows; n_cols_ = n_cols; g.pr0 = ro_s; g.pc0 = co_s; }
+    if (next_state) {   // state returned by fill_dense_submat_impl (:166-169)
+        const int64_t ptr = (nat == 'C') ? ro_s + co_s * L : ro_s * L + co_s;
+        const int64_t pad = (L % 4) ? 4 - L % 4 : 0;
+        const int64_t ptr_padded = ptr + ptr / L * pad;
+        *next_state = *seed;
+        rb::ctr_add(seed->counter, (uint64_t)(ptr_padded / 4 + n_rows_ * (int64_t)g.stride), next_state->counter);
+    }
+    hipStream_t s = (hipStream_t)stream;
+    Stager st(s);
+    void *dbuf;
+    RBH_HIP(st.map(buff, sizeof(T) * n_rows * n_cols, false, true, &dbuf));
+    RBH_HIP(launch_fill_t<T>(g, n_rows_, n_cols_, layout != nat, (T *)dbuf, s));
+    RBH_HIP(st.finish());
+    return RBH_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// sparse
+// ---------------------------------------------------------------------------------------------
+int64_t sparse_nnz(const rbh_sparse_dist *D) {   // sparse_skops.hh:351-360
+    const int64_t mx = std::max(D->n_rows, D->n_cols), mn = std::min(D->n_rows, D->n_cols);
+    return D->vec_nnz * (D->major_axis == 'S' ? mx : mn);
+}
+
+template <typename T> hipError_t launch_fill_sparse_t(const SparseGen &, int64_t *, int64_t *, T *, hipStream_t);
+template <> hipError_t launch_fill_sparse_t<double>(const SparseGen &g, int64_t *r, int64_t *c, double *v, hipStream_t s) {
+    return launch_fill_sparse_f64(g, r, c, v, s);
+}
+template <> hipError_t launch_fill_sparse_t<float>(const SparseGen &g, int64_t *r, int64_t *c, float *v, hipStream_t s) {
+    return launch_fill_sparse_f32(g, r, c, v, s);
+}
+template <typename T>
+hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *r, const int64_t *c, const T *v, int64_t nnz,
+                              hipStream_t s);
+template <>
+hipError_t run_sparse_apply_t<double>(const SparseApply &p, const int64_t *r, const int64_t *c, const double *v,
+                                      int64_t nnz, hipStream_t s) {
+    return run_sparse_apply_f64(p, r, c, v, nnz, s);
+}
+template <>
+hipError_t run_sparse_apply_t<float>(const SparseApply &p, const int64_t *r, const int64_t *c, const float *v,
+                                     int64_t nnz, hipStream_t s) {
+    return run_sparse_apply_f32(p, r, c, v, nnz, s);
+}
+
+SparseGen make_sparse_gen(const rbh_sparse_dist *D, const rbh_state *seed) {
+    SparseGen g{};
+    g.n_rows = D->n_rows;
+    g.n_cols = D->n_cols;
+    g.vec_nnz = D->vec_nnz;
+    g.major_axis = D->major_axis;
+    memcpy(g.ctr, seed->counter, sizeof g.ctr);
+    memcpy(g.key, seed->key, sizeof g.key);
+    return g;
+}
+
+int check_sparse_dist(const rbh_sparse_dist *D) {
+    RBH_REQUIRE(D != nullptr);
+    RBH_REQUIRE(D->n_rows > 0);
+    RBH_REQUIRE(D->n_cols > 0);
+    RBH_REQUIRE(D->vec_nnz > 0);
+    RBH_REQUIRE(D->major_axis == 'S' || D->major_axis == 'L');
+    const int64_t dim_major = D->major_axis == 'S' ? std::min(D->n_rows, D->n_cols) : std::max(D->n_rows, D->n_cols);
+    if (D->vec_nnz > dim_major)   // randblas_error_if(vec_nnz > dim_major) (sparse_skops.hh:64)
+        return set_error(RBH_ERR_REQUIRE, "vec_nnz > dim_major, in function repeated_fisher_yates");
+    return RBH_OK;
+}
+
+template <typename T>
+int fill_sparse(const rbh_sparse_dist *D, const rbh_state *seed, int64_t *rows, int64_t *cols, T *vals,
+                void *stream) {
+    int rc = check_sparse_dist(D);
+    if (rc) return rc;
+    RBH_REQUIRE(seed != nullptr && rows != nullptr && cols != nullptr);
+    const int64_t nnz = sparse_nnz(D);
+    hipStream_t s = (hipStream_t)stream;
+    Stager st(s);
+    void *dr, *dc, *dv;
+    RBH_HIP(st.map(rows, sizeof(int64_t) * nnz, false, true, &dr));
+    RBH_HIP(st.map(cols, sizeof(int64_t) * nnz, false, true, &dc));
+    RBH_HIP(st.map(vals, sizeof(T) * nnz, false, true, &dv));
+    RBH_HIP(launch_fill_sparse_t<T>(make_sparse_gen(D, seed), (int64_t *)dr, (int64_t *)dc, (T *)dv, s));
+    RBH_HIP(st.finish());
+    return RBH_OK;
+}
+
+// The reference's left_spmm dimension / leading-dimension checks (spmm_dispatch.hh:96-121),
+// after the opS == Trans transposition of the COO view (:69-87).
+int check_left_spmm(char layout, char opS, char opB, int64_t d, int64_t n, int64_t m, const rbh_sparse_dist *D,
+                    int64_t ldb, int64_t ldc) {
+    const int64_t A_rows = opS == 'N' ? D->n_rows : D->n_cols;
+    const int64_t A_cols = opS == 'N' ? D->n_cols : D->n_rows;
+    RBH_REQUIRE(A_rows >= d);
+    RBH_REQUIRE(A_cols >= m);
+    const int64_t rows_B = opB == 'N' ? m : n, cols_B = opB == 'N' ? n : m;
+    if (layout == 'C') {
+        RBH_REQUIRE(ldb >= rows_B);
+        RBH_REQUIRE(ldc >= d);
+    } else {
+        RBH_REQUIRE(ldc >= n);
+        RBH_REQUIRE(ldb >= cols_B);
+    }
+    return RBH_OK;
+}
+
+template <typename T>
+int sparse_common(SparseApply &p, const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz, const int64_t *rows,
+                  const int64_t *cols, const T *vals, const T *A, int64_t A_extent, T *B, int64_t B_extent,
+                  T beta, hipStream_t s) {
+    Stager st(s);
+    void *dA, *dB;
+    RBH_HIP(st.map(A, sizeof(T) * A_extent, true, false, &dA));
+    RBH_HIP(st.map(B, sizeof(T) * B_extent, beta != (T)0, true, &dB));
+    p.Y = dA;
+    p.C = dB;
+    const void *dr = nullptr, *dc = nullptr, *dv = nullptr;
+    void *gen_ws = nullptr;
+    if (!rows) {   // sample the operator on the device
+        RBH_REQUIRE(seed != nullptr);
+        nnz = sparse_nnz(D);
+        const size_t bytes = (size_t)nnz * (2 * sizeof(int64_t) + sizeof(T));
+        RBH_HIP(hipMallocAsync(&gen_ws, bytes, s));
+        int64_t *gr = (int64_t *)gen_ws;
+        int64_t *gc = gr + nnz;
+        T *gv = (T *)(gc + nnz);
+        RBH_HIP(launch_fill_sparse_t<T>(make_sparse_gen(D, seed), gr, gc, gv, s));
+        dr = gr; dc = gc; dv = gv;
+    } else {
+        RBH_REQUIRE(cols != nullptr && vals != nullptr && nnz >= 0);
+        void *t0, *t1, *t2;
+        RBH_HIP(st.map(rows, sizeof(int64_t) * nnz, true, false, &t0));
+        RBH_HIP(st.map(cols, sizeof(int64_t) * nnz, true, false, &t1));
+        RBH_HIP(st.map(vals, sizeof(T) * nnz, true, false, &t2));
+        dr = t0; dc = t1; dv = t2;
+    }
+    if (p.alpha == 0.0) nnz = 0;   // left_spmm returns after the beta scaling (:134-135)
+    hipError_t e = run_sparse_apply_t<T>(p, (const int64_t *)dr, (const int64_t *)dc, (const T *)dv, nnz, s);
+    if (gen_ws) (void)hipFreeAsync(gen_ws, s);
+    RBH_HIP(e);
+    RBH_HIP(st.finish());
+    return RBH_OK;
+}
+
+// left: B = alpha op(submat(S)) op(A) + beta B   (sparse::lskges, skge.hh:485-510)
+template <typename T>
+int lskges(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, T alpha, const rbh_sparse_dist *D,
+           const rbh_state *seed, int64_t nnz, const int64_t *rows, const int64_t *cols, const T *vals, int64_t ro_s,
+           int64_t co_s, const T *A, int64_t lda, T beta, T *B, int64_t ldb, void *stream) {
+    RBH_REQUIRE(layout == 'C' || layout == 'R');
+    RBH_REQUIRE(opS == 'N' || opS == 'T');
+    RBH_REQUIRE(opA == 'N' || opA == 'T');
+    int rc = check_sparse_dist(D);
+    if (rc) return rc;
+    RBH_REQUIRE(d >= 0 && n >= 0 && m >= 0 && ro_s >= 0 && co_s >= 0);
+    rc = check_left_spmm(layout, opS, opA, d, n, m, D, lda, ldb);
+    if (rc) return rc;
+    SparseApply p{};
+    p.M = d; p.N = n; p.K = m;
+    p.alpha = alpha; p.beta = beta;
+    p.ro = ro_s; p.co = co_s;
+    p.transposed = opS == 'T';
+    p.win_r = opS == 'N' ? d : m;
+    p.win_c = opS == 'N' ? m : d;
+    const bool col = layout == 'C';
+    p.crs = col ? 1 : ldb;
+    p.ccs = col ? ldb : 1;
+    if (col) { p.ysk = opA == 'N' ? 1 : lda; p.ysj = opA == 'N' ? lda : 1; }
+    else { p.ysk = opA == 'N' ? lda : 1; p.ysj = opA == 'N' ? 1 : lda; }
+    const int64_t rows_A = opA == 'N' ? m : n, cols_A = opA == 'N' ? n : m;
+    return sparse_common<T>(p, D, seed, nnz, rows, cols, vals, A, extent(layout, rows_A, cols_A, lda), B,
+                            extent(layout, d, n, ldb), beta, (hipStream_t)stream);
+}
+
+// right: B = alpha op(A) op(submat(S)) + beta B   (sparse::rskges, skge.hh:616-641 -> right_spmm,
+// spmm_dispatch.hh:162-200, which calls left_spmm(trans_layout, trans_opS, opA, d, m, n, ...))
+template <typename T>
+int rskges(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, T alpha, const T *A, int64_t lda,
+           const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz, const int64_t *rows, const int64_t *cols,
+           const T *vals, int64_t ro_s, int64_t co_s, T beta, T *B, int64_t ldb, void *stream) {
+    RBH_REQUIRE(layout == 'C' || layout == 'R');
+    RBH_REQUIRE(opS == 'N' || opS == 'T');
+    RBH_REQUIRE(opA == 'N' || opA == 'T');
+    int rc = check_sparse_dist(D);
+    if (rc) return rc;
+    RBH_REQUIRE(d >= 0 && n >= 0 && m >= 0 && ro_s >= 0 && co_s >= 0);
+    const char tlayout = layout == 'C' ? 'R' : 'C';
+    const char topS = opS == 'N' ? 'T' : 'N';
+    rc = check_left_spmm(tlayout, topS, opA, d, m, n, D, lda, ldb);
+    if (rc) return rc;
+    SparseApply p{};
+    p.M = d; p.N = m; p.K = n;
+    p.alpha = alpha; p.beta = beta;
+    p.ro = ro_s; p.co = co_s;
+    p.transposed = opS == 'N';   // operator element (i over d, k over n) = op(submat S)(k, i)
+    p.win_r = opS == 'N' ? n : d;
+    p.win_c = opS == 'N' ? d : n;
+    const bool col = layout == 'C';
+    // C(i, j) = B(j, i)
+    p.crs = col ? ldb : 1;
+    p.ccs = col ? 1 : ldb;
+    // Y(k, j) = op(A)(j, k)
+    if (col) { p.ysk = opA == 'N' ? lda : 1; p.ysj = opA == 'N' ? 1 : lda; }
+    else { p.ysk = opA == 'N' ? 1 : lda; p.ysj = opA == 'N' ? lda : 1; }
+    const int64_t rows_A = opA == 'N' ? m : n, cols_A = opA == 'N' ? n : m;
+    return sparse_common<T>(p, D, seed, nnz, rows, cols, vals, A, extent(layout, rows_A, cols_A, lda), B,
+                            extent(layout, m, d, ldb), beta, (hipStream_t)stream);
+}
+
+template <typename T> hipError_t launch_sym_t(char, const T *, int64_t, int64_t, T, int *, hipStream_t);
+template <> hipError_t launch_sym_t<double>(char l, const double *A, int64_t n, int64_t lda, double tol, int *f, hipStream_t s) {
+    return launch_symcheck_f64(l, A, n, lda, tol, f, s);
+}
+template <> hipError_t launch_sym_t<float>(char l, const float *A, int64_t n, int64_t lda, float tol, int *f, hipStream_t s) {
+    return launch_symcheck_f32(l, A, n, lda, tol, f, s);
+}
+
+template <typename T>
+int require_symmetric(char layout, const T *A, int64_t n, int64_t lda, T tol, void *stream) {
+    if (tol < 0) return RBH_OK;   // util.hh:166-168
+    RBH_REQUIRE(layout == 'C' || layout == 'R');
+    RBH_REQUIRE(n >= 0 && lda >= n);
+    hipStream_t s = (hipStream_t)stream;
+    Stager st(s);
+    void *dA;
+    RBH_HIP(st.map(A, sizeof(T) * extent(layout, n, n, lda), true, false, &dA));
+    int *flag = nullptr;
+    RBH_HIP(hipMallocAsync((void **)&flag, sizeof(int), s));
+    RBH_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
+    RBH_HIP(launch_sym_t<T>(layout, (const T *)dA, n, lda, tol, flag, s));
+    int h = 0;
+    RBH_HIP(hipMemcpyAsync(&h, flag, sizeof(int), hipMemcpyDeviceToHost, s));
+    RBH_HIP(hipFreeAsync(flag, s));
+    RBH_HIP(hipStreamSynchronize(s));
+    RBH_HIP(st.finish());
+    if (h) return set_error(RBH_ERR_SYMMETRY, "Symmetry check failed, in function require_symmetric");
+    return RBH_OK;
+}
+
+}  // namespace
+
+// =============================================================================================
+// extern "C" surface
+// =============================================================================================
+extern "C" {
+
+int rbh_abi_version(void) { return 1; }
+const char *rbh_last_error(void) { return g_last_error.c_str(); }
+
+int rbh_dense_next_state(const rbh_dense_dist *D, const rbh_state *seed, rbh_state *next) {
+    RBH_REQUIRE(D && seed && next);
+    dense_next(D, seed, next);
+    return RBH_OK;
+}
+
+int rbh_sparse_next_state(const rbh_sparse_dist *D, const rbh_state *seed, rbh_state *next) {
+    RBH_REQUIRE(D && seed && next);
+    // sparse::compute_next_state (sparse_skops.hh:115-126): advances by vec_nnz * minor_len with
+    // minor_len = min(dims) for SASO, max(dims) for LASO (reference quirk kept).
+    const int64_t minor_len = D->major_axis == 'S' ? std::min(D->n_rows, D->n_cols) : std::max(D->n_rows, D->n_cols);
+    *next = *seed;
+    rb::ctr_add(seed->counter, (uint64_t)(minor_len * D->vec_nnz), next->counter);
+    return RBH_OK;
+}
+
+int64_t rbh_sparse_nnz(const rbh_sparse_dist *D) { return D ? sparse_nnz(D) : -1; }
+
+int rbh_fill_dense_f64(char layout, const rbh_dense_dist *D, int64_t n_rows, int64_t n_cols, int64_t ro_s,
+                       int64_t co_s, double *buff, const rbh_state *seed, rbh_state *next_state, void *stream) {
+    return fill_dense<double>(layout, D, n_rows, n_cols, ro_s, co_s, buff, seed, next_state, stream);
+}
+int rbh_fill_dense_f32(char layout, const rbh_dense_dist *D, int64_t n_rows, int64_t n_cols, int64_t ro_s,
+                       int64_t co_s, float *buff, const rbh_state *seed, rbh_state *next_state, void *stream) {
+    return fill_dense<float>(layout, D, n_rows, n_cols, ro_s, co_s, buff, seed, next_state, stream);
+}
+
+int rbh_fill_sparse_f64(const rbh_sparse_dist *D, const rbh_state *seed, int64_t *rows, int64_t *cols, double *vals,
+                        void *stream) {
+    return fill_sparse<double>(D, seed, rows, cols, vals, stream);
+}
+int rbh_fill_sparse_f32(const rbh_sparse_dist *D, const rbh_state *seed, int64_t *rows, int64_t *cols, float *vals,
+                        void *stream) {
+    return fill_sparse<float>(D, seed, rows, cols, vals, stream);
+}
+
+int rbh_lskge3_f64(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, double alpha,
+                   const rbh_dense_dist *D, const rbh_state *seed, const double *S_buff, char S_layout, int64_t ro_s,
+                   int64_t co_s, const double *A, int64_t lda, double beta, double *B, int64_t ldb, void *stream) {
+    return lskge3<double>(layout, opS, opA, d, n, m, alpha, D, seed, S_buff, S_layout, ro_s, co_s, A, lda, beta, B,
+                          ldb, stream);
+}
+int rbh_lskge3_f32(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, float alpha,
+                   const rbh_dense_dist *D, const rbh_state *seed, const float *S_buff, char S_layout, int64_t ro_s,
+                   int64_t co_s, const float *A, int64_t lda, float beta, float *B, int64_t ldb, void *stream) {
+    return lskge3<float>(layout, opS, opA, d, n, m, alpha, D, seed, S_buff, S_layout, ro_s, co_s, A, lda, beta, B,
+                         ldb, stream);
+}
+int rbh_rskge3_f64(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, double alpha, const double *A,
+                   int64_t lda, const rbh_dense_dist *D, const rbh_state *seed, const double *S_buff, char S_layout,
+                   int64_t ro_s, int64_t co_s, double beta, double *B, int64_t ldb, void *stream) {
+    return rskge3<double>(layout, opA, opS, m, d, n, alpha, A, lda, D, seed, S_buff, S_layout, ro_s, co_s, beta, B,
+                          ldb, stream);
+}
+int rbh_rskge3_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, float alpha, const float *A,
+                   int64_t lda, const rbh_dense_dist *D, const rbh_state *seed, const float *S_buff, char S_layout,
+                   int64_t ro_s, int64_t co_s, float beta, float *B, int64_t ldb, void *stream) {
+    return rskge3<float>(layout, opA, opS, m, d, n, alpha, A, lda, D, seed, S_buff, S_layout, ro_s, co_s, beta, B,
+                         ldb, stream);
+}
+
+int rbh_lskges_f64(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, double alpha,
+                   const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz, const int64_t *rows,
+                   const int64_t *cols, const double *vals, int64_t ro_s, int64_t co_s, const double *A, int64_t lda,
+                   double beta, double *B, int64_t ldb, void *stream) {
+    return lskges<double>(layout, opS, opA, d, n, m, alpha, D, seed, nnz, rows, cols, vals, ro_s, co_s, A, lda, beta,
+                          B, ldb, stream);
+}
+int rbh_lskges_f32(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, float alpha,
+                   const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz, const int64_t *rows,
+                   const int64_t *cols, const float *vals, int64_t ro_s, int64_t co_s, const float *A, int64_t lda,
+                   float beta, float *B, int64_t ldb, void *stream) {
+    return lskges<float>(layout, opS, opA, d, n, m, alpha, D, seed, nnz, rows, cols, vals, ro_s, co_s, A, lda, beta,
+                         B, ldb, stream);
+}
+int rbh_rskges_f64(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, double alpha, const double *A,
+                   int64_t lda, const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz, const int64_t *rows,
+                   const int64_t *cols, const double *vals, int64_t ro_s, int64_t co_s, double beta, double *B,
+                   int64_t ldb, void *stream) {
+    return rskges<double>(layout, opA, opS, m, d, n, alpha, A, lda, D, seed, nnz, rows, cols, vals, ro_s, co_s, beta,
+                          B, ldb, stream);
+}
+int rbh_rskges_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, float alpha, const float *A,
+                   int64_t lda, const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz, const int64_t *rows,
+                   const int64_t *cols, const float *vals, int64_t ro_s, int64_t co_s, float beta, float *B,
+                   int64_t ldb, void *stream) {
+    return rskges<float>(layout, opA, opS, m, d, n, alpha, A, lda, D, seed, nnz, rows, cols, vals, ro_s, co_s, beta,
+                         B, ldb, stream);
+}
+
+int rbh_require_symmetric_f64(char layout, const double *A, int64_t n, int64_t lda, double tol, void *stream) {
+    return require_symmetric<double>(layout, A, n, lda, tol, stream);
+}
+int rbh_require_symmetric_f32(char layout, const float *A, int64_t n, int64_t lda, float tol, void *stream) {
+    return require_symmetric<float>(layout, A, n, lda, tol, stream);
+}
+
+}  // extern "C"

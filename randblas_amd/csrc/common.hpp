@@ -1,0 +1,67 @@
+// common.hpp -- shared host/device declarations for librandblas_hip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "rng_core.hpp"
+
+namespace rbh {
+
+// ------------------------------------------------------------------------------------------
+// Operand descriptors of the canonical device GEMM
+//      C[M x N] (col-major, ldc) = alpha * X[M x K] * Y[K x N] + beta * C.
+// Both X and Y are addressed by (o, k): o = outer index (row i of X, column j of Y), k = the
+// contracted index. An operand is either a strided memory matrix or a window of a RandBLAS dense
+// sketching operator regenerated on the fly from its Philox counter (never stored in HBM).
+// ------------------------------------------------------------------------------------------
+enum OpKind : int {
+    MEM = 0,      // element (o,k) = ptr[o*so + k*sk]
+    GEN_OK = 1,   // element (o,k) = P(pr0 + o, pc0 + k): Philox counter runs along k
+    GEN_OO = 2,   // element (o,k) = P(pr0 + k, pc0 + o): Philox counter runs along o
+};
+
+// P(pr, pc) = sample[pc & 3] of Philox4x32-10(ctr + pr*stride + (pc >> 2), key), i.e. entry
+// (pr, pc) of the operator's natural row-major parent (RandBLAS/dense_skops.hh:109-162 with
+// the layout map of :494-503).
+struct GenOperand {
+    uint32_t ctr[4];
+    uint32_t key[2];
+    uint64_t stride;     // counters per natural row = ceil(L / 4), L = major-axis length
+    int64_t pr0, pc0;    // natural coordinates of operand element (0, 0)
+    int family;          // rb::GAUSSIAN / rb::UNIFORM
+    double scale;        // uniform: (T)sqrt(3) multiplier (dense_skops.hh:510-513); 1 otherwise
+};
+
+struct MemOperand {
+    const void *ptr;
+    int64_t so, sk;
+};
+
+struct GemmProblem {
+    int64_t M, N, K;
+    double alpha, beta;
+    void *C;
+    int64_t ldc;
+    int xkind, ykind;
+    int xmode, ymode;    // MEM load mode: 2 = 16-B loads along k, 1 = scalar along k, 0 = scalar along o
+    MemOperand xm, ym;
+    GenOperand xg, yg;
+};
+
+// Kernel launchers (skge_dense.hip)
+hipError_t launch_gemm_f64(const GemmProblem &p, hipStream_t s);
+hipError_t launch_gemm_f32(const GemmProblem &p, hipStream_t s);
+// C = beta*C over an M x N col-major matrix (beta == 0 writes zeros; util::safe_scal semantics)
+hipError_t launch_scale_f64(int64_t M, int64_t N, double beta, double *C, int64_t ldc, hipStream_t s);
+hipError_t launch_scale_f32(int64_t M, int64_t N, float beta, float *C, int64_t ldc, hipStream_t s);
+
+// fill_dense on device (fill_dense.hip): write the n_rows_ x n_cols_ row-major window of the
+// natural parent (row length L) starting at natural (pr0, pc0) into buff, either as-is
+// (transpose_out == 0: buff[r*n_cols_ + c]) or transposed (buff[c*n_rows_ + r]).
+hipError_t launch_fill_dense_f64(const GenOperand &g, int64_t n_rows_, int64_t n_cols_, int transpose_out,
+                                 double *buff, hipStream_t s);
+hipError_t launch_fill_dense_f32(const GenOperand &g, int64_t n_rows_, int64_t n_cols_, int transpose_out,
+                                 float *buff, hipStream_t s);
+
+}  // namespace rbh

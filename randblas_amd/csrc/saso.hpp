@@ -1,0 +1,43 @@
+// saso.hpp -- host-side descriptors of the sparse-operator kernels (saso.hip).
+#pragma once
+#include "common.hpp"
+
+namespace rbh {
+
+// SparseDist + seed (sparse_skops.hh:134-165, 183-377).
+struct SparseGen {
+    int64_t n_rows, n_cols, vec_nnz;
+    char major_axis;   // 'S' (SASO) or 'L' (LASO)
+    uint32_t ctr[4];
+    uint32_t key[2];
+};
+
+// Canonical sparse apply: C (M x N, element (i,j) at C[i*crs + j*ccs]) =
+//   beta*C + op'(window of S) (M x K, alpha folded into the values) * Y (K x N, (k,j) at Y[k*ysk + j*ysj]).
+// The window is S[ro : ro+win_r, co : co+win_c]; transposed = 1 means operator element (i, k) is
+// window element (k, i).
+struct SparseApply {
+    int64_t M, N, K;
+    double alpha, beta;
+    int64_t ro, co, win_r, win_c;
+    int transposed;
+    const void *Y;
+    int64_t ysk, ysj;
+    void *C;
+    int64_t crs, ccs;
+};
+
+hipError_t launch_fill_sparse_f64(const SparseGen &g, int64_t *rows, int64_t *cols, double *vals, hipStream_t s);
+hipError_t launch_fill_sparse_f32(const SparseGen &g, int64_t *rows, int64_t *cols, float *vals, hipStream_t s);
+hipError_t run_sparse_apply_f64(const SparseApply &p, const int64_t *rows, const int64_t *cols, const double *vals,
+                                int64_t nnz, hipStream_t s);
+hipError_t run_sparse_apply_f32(const SparseApply &p, const int64_t *rows, const int64_t *cols, const float *vals,
+                                int64_t nnz, hipStream_t s);
+
+// util::require_symmetric on the device (sksy.hip). Writes 0/1 (violation found) to *flag.
+hipError_t launch_symcheck_f64(char layout, const double *A, int64_t n, int64_t lda, double tol, int *flag,
+                               hipStream_t s);
+hipError_t launch_symcheck_f32(char layout, const float *A, int64_t n, int64_t lda, float tol, int *flag,
+                               hipStream_t s);
+
+}  // namespace rbh

@@ -1,0 +1,349 @@
+// skge_dense.hip -- fused Philox/Box-Muller + MFMA GEMM for RandBLAS dense sketching (gfx950).
+//
+// Replaces the reference's two-step dense path, dense::lskge3 / rskge3 (RandBLAS/skge.hh:173-215,
+// :320-364): "sample submat(S) into a host buffer with fill_dense (dense_skops.hh:96-170), then
+// blas::gemm (skge.hh:213, :362)". Here the operator window is regenerated tile by tile from its
+// Philox counters straight into LDS, next to the MFMA consumer, so S is never written to HBM.
+//
+// Canonical problem: C[M x N] (col-major) = alpha * X[M x K] * Y[K x N] + beta * C, with X and Y
+// each a strided memory matrix or a generated operator window (common.hpp). The host side
+// (capi.cpp) reduces every {left, right} x {ColMajor, RowMajor} x {opS, opA} case to it.
+//
+// Work decomposition (one workgroup = 8 waves = 512 threads, one output tile BM x BN):
+//   * K is walked in steps of BK = 16. Per step the X tile (BM x 16) and Y tile (BN x 16) are
+//     staged in LDS as [outer][k] rows padded to 144 B (f64) / 80 B (f32); two stages.
+//   * A generated tile costs BM*BK/4 Philox calls: one call yields 4 consecutive entries of a
+//     natural row (GEN_OK: 4 consecutive k; GEN_OO: 4 consecutive outer indices).
+//   * Each wave owns a 64 x 64 sub-tile = 4 x 4 MFMA 16x16x4 tiles (f64: 128 accumulator VGPRs).
+//     Lane (g = lane>>4, r = lane&15) reads 4 consecutive k (4g..4g+3) of row r of its X and Y
+//     fragments with one 32-B (f64) / 16-B (f32) LDS read and issues 4 MFMAs, the s-th contracting
+//     k = 4g+s. The k order inside a step is thereby permuted, identically for both operands.
+//   * The MFMA takes Y as its A operand and X as its B operand, so each accumulator register holds
+//     16 consecutive output rows i across lanes: the col-major epilogue stores 128-B runs.
+//   * Tiles are numbered output-row-fastest and dealt XCD-contiguously (bijective remap), so the
+//     row tiles that share one Y column panel run on one XCD and share its L2.
+#include "common.hpp"
+
+namespace rbh {
+
+constexpr int BK = 16;
+
+template <typename T> struct Mfma;
+template <> struct Mfma<double> {
+    typedef double v4 __attribute__((ext_vector_type(4)));
+    static constexpr int LDK = BK + 2;   // 144-B rows: 16 lanes' 32-B reads hit distinct bank quads
+    __device__ static inline v4 mma(double a, double b, v4 c) {
+        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    }
+    // accumulator register reg of lane -> row of the MFMA result (= output column offset j)
+    __device__ static inline int drow(int lane, int reg) { return (lane >> 4) + 4 * reg; }
+};
+template <> struct Mfma<float> {
+    typedef float v4 __attribute__((ext_vector_type(4)));
+    static constexpr int LDK = BK + 4;   // 80-B rows
+    __device__ static inline v4 mma(float a, float b, v4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    __device__ static inline int drow(int lane, int reg) { return (lane >> 4) * 4 + reg; }
+};
+
+// ------------------------------------------------------------------------------------------
+// Generated operand tile -> LDS
+// ------------------------------------------------------------------------------------------
+template <typename T, int FAMILY>
+__device__ __forceinline__ void gen_call(const GenOperand &g, uint64_t off, T out[4]) {
+    uint32_t c[4];
+    rb::ctr_add(g.ctr, off, c);
+    const rb::u32x4 w = rb::philox4x32<10>(c[0], c[1], c[2], c[3], g.key[0], g.key[1]);
+    float s[4];
+    rb::sample4<FAMILY>(w, s);
+    if (FAMILY == rb::UNIFORM) {
+        const T sc = (T)g.scale;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) out[e] = (T)s[e] * sc;
+    } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) out[e] = (T)s[e];
+    }
+}
+
+// Fill lds[o * LDK + k] (o < NO, k < BK) with operand elements (o0 + o, k0 + k); elements outside
+// [0, nO) x [0, K) are zero.
+template <typename T, int KIND, int FAMILY, int NO, int NT>
+__device__ __forceinline__ void gen_tile(const GenOperand &g, int64_t o0, int64_t k0, int64_t nO, int64_t K,
+                                         T *lds, int tid) {
+    constexpr int LDK = Mfma<T>::LDK;
+    if (KIND == GEN_OK) {
+        const int64_t pcs = g.pc0 + k0;
+        const int64_t qa = pcs >> 2;
+        const int nq = (int)(((pcs + BK - 1) >> 2) - qa + 1);
+        const int ncalls = NO * nq;
+#pragma unroll 1
+        for (int c = tid; c < ncalls; c += NT) {
+            const int o = c / nq;
+            const int64_t q = qa + (c - o * nq);
+            T v[4];
+            gen_call<T, FAMILY>(g, (uint64_t)(g.pr0 + o0 + o) * g.stride + (uint64_t)q, v);
+            const bool orow = (o0 + o) < nO;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int k = (int)(4 * q + e - pcs);
+                if (k >= 0 && k < BK) lds[o * LDK + k] = (orow && k0 + k < K) ? v[e] : (T)0;
+            }
+        }
+    } else {
+        const int64_t pcs = g.pc0 + o0;
+        const int64_t qa = pcs >> 2;
+        const int nq = (int)(((pcs + NO - 1) >> 2) - qa + 1);
+        const int ncalls = BK * nq;
+#pragma unroll 1
+        for (int c = tid; c < ncalls; c += NT) {
+            const int k = c / nq;
+            const int64_t q = qa + (c - k * nq);
+            T v[4];
+            gen_call<T, FAMILY>(g, (uint64_t)(g.pr0 + k0 + k) * g.stride + (uint64_t)q, v);
+            const bool kin = (k0 + k) < K;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int o = (int)(4 * q + e - pcs);
+                if (o >= 0 && o < NO) lds[o * LDK + k] = (kin && o0 + o < nO) ? v[e] : (T)0;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Memory operand tile: global -> registers (issued one step ahead) -> LDS
+// ------------------------------------------------------------------------------------------
+template <typename T> struct Vec2;
+template <> struct Vec2<double> { typedef double type __attribute__((ext_vector_type(2))); };
+template <> struct Vec2<float> { typedef float type __attribute__((ext_vector_type(4))); };
+
+template <typename T, int NO, int NT>
+struct MemTile {
+    static constexpr int EPT = NO * BK / NT;          // elements per thread
+    static constexpr int VEC = 16 / (int)sizeof(T);   // elements per 16-B load
+    static constexpr int NV = EPT / VEC;
+    typedef typename Vec2<T>::type v_t;
+    T v[EPT];
+    // mode 2: 16-B loads along k (operand contiguous along k, 16-B aligned rows, K % VEC == 0)
+    // mode 1: scalar loads, consecutive threads walk k; mode 0: scalar loads walking o.
+    __device__ __forceinline__ void load(const MemOperand &m, int64_t o0, int64_t k0, int64_t nO, int64_t K,
+                                         int tid, int mode) {
+        const T *p = (const T *)m.ptr;
+        if (mode == 2) {
+#pragma unroll
+            for (int e = 0; e < NV; ++e) {
+                const int idx = tid + e * NT;
+                const int o = idx / (BK / VEC);
+                const int k = (idx % (BK / VEC)) * VEC;
+                const int64_t go = o0 + o, gk = k0 + k;
+                v_t x;
+                if (go < nO && gk < K) x = *reinterpret_cast<const v_t *>(p + go * m.so + gk);
+                else for (int q = 0; q < VEC; ++q) x[q] = (T)0;
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) v[e * VEC + q] = x[q];
+            }
+            return;
+        }
+        const bool kfast = mode == 1;
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) {
+            const int idx = tid + e * NT;
+            const int o = kfast ? idx / BK : idx % NO;
+            const int k = kfast ? idx % BK : idx / NO;
+            const int64_t go = o0 + o, gk = k0 + k;
+            v[e] = (go < nO && gk < K) ? p[go * m.so + gk * m.sk] : (T)0;
+        }
+    }
+    __device__ __forceinline__ void store(T *lds, int tid, int mode) const {
+        constexpr int LDK = Mfma<T>::LDK;
+        if (mode == 2) {
+#pragma unroll
+            for (int e = 0; e < NV; ++e) {
+                const int idx = tid + e * NT;
+                const int o = idx / (BK / VEC);
+                const int k = (idx % (BK / VEC)) * VEC;
+                v_t x;
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) x[q] = v[e * VEC + q];
+                *reinterpret_cast<v_t *>(lds + o * LDK + k) = x;
+            }
+            return;
+        }
+        const bool kfast = mode == 1;
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) {
+            const int idx = tid + e * NT;
+            const int o = kfast ? idx / BK : idx % NO;
+            const int k = kfast ? idx % BK : idx / NO;
+            lds[o * LDK + k] = v[e];
+        }
+    }
+};
+
+
+// ------------------------------------------------------------------------------------------
+// The kernel
+// ------------------------------------------------------------------------------------------
+template <typename T, int XK, int YK, int FAMILY, int BM, int BN, int WAVES_M, int WAVES_N>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void skge_gemm_kernel(const GemmProblem p) {
+    constexpr int NT = 64 * WAVES_M * WAVES_N;
+    constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
+    constexpr int FA = WM / 16, FB = WN / 16;
+    constexpr int LDK = Mfma<T>::LDK;
+    constexpr int XS = BM * LDK, YS = BN * LDK;
+    typedef typename Mfma<T>::v4 acc_t;
+
+    __shared__ __attribute__((aligned(16))) T lds[2 * (XS + YS)];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave % WAVES_M, wn = wave / WAVES_M;
+
+    // XCD-aware bijective tile remap: logical tiles [x*q, ...) go to the blocks of XCD group x.
+    const int64_t nTm = (p.M + BM - 1) / BM, nTn = (p.N + BN - 1) / BN;
+    const int64_t nb = nTm * nTn;
+    const int64_t b = blockIdx.x;
+    const int64_t xcd = b % 8, qq = nb / 8, rr = nb % 8;
+    const int64_t t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + b / 8;
+    const int64_t tm = t % nTm, tn = t / nTm;
+    const int64_t i0 = tm * BM, j0 = tn * BN;
+
+    const int xmode = (XK == MEM) ? p.xmode : 0;
+    const int ymode = (YK == MEM) ? p.ymode : 0;
+
+    MemTile<T, BM, NT> xt;
+    MemTile<T, BN, NT> yt;
+
+    acc_t acc[FA][FB];
+#pragma unroll
+    for (int a = 0; a < FA; ++a)
+#pragma unroll
+        for (int c = 0; c < FB; ++c) acc[a][c] = (acc_t){0, 0, 0, 0};
+
+    const int64_t nk = (p.K + BK - 1) / BK;
+
+    // prologue: stage 0
+    if (XK == MEM) { xt.load(p.xm, i0, 0, p.M, p.K, tid, xmode); xt.store(lds, tid, xmode); }
+    else gen_tile<T, XK, FAMILY, BM, NT>(p.xg, i0, 0, p.M, p.K, lds, tid);
+    if (YK == MEM) { yt.load(p.ym, j0, 0, p.N, p.K, tid, ymode); yt.store(lds + XS, tid, ymode); }
+    else gen_tile<T, YK, FAMILY, BN, NT>(p.yg, j0, 0, p.N, p.K, lds + XS, tid);
+    __syncthreads();
+
+    const int g4 = (lane >> 4) * 4;
+    const int r = lane & 15;
+
+    for (int64_t kt = 0; kt < nk; ++kt) {
+        const int cur = (int)(kt & 1);
+        T *Xc = lds + cur * (XS + YS);
+        T *Yc = Xc + XS;
+        T *Xn = lds + (cur ^ 1) * (XS + YS);
+        T *Yn = Xn + XS;
+        const bool more = kt + 1 < nk;
+        const int64_t kn = (kt + 1) * BK;
+        if (more) {
+            if (XK == MEM) xt.load(p.xm, i0, kn, p.M, p.K, tid, xmode);
+            if (YK == MEM) yt.load(p.ym, j0, kn, p.N, p.K, tid, ymode);
+        }
+        // ---- MFMA on the current stage: 4 sub-steps, sub-step s contracts k = 4g + s
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            T xf[FA], yf[FB];
+#pragma unroll
+            for (int a = 0; a < FA; ++a) xf[a] = Xc[(wm * WM + 16 * a + r) * LDK + g4 + s];
+#pragma unroll
+            for (int c = 0; c < FB; ++c) yf[c] = Yc[(wn * WN + 16 * c + r) * LDK + g4 + s];
+#pragma unroll
+            for (int a = 0; a < FA; ++a)
+#pragma unroll
+                for (int c = 0; c < FB; ++c) acc[a][c] = Mfma<T>::mma(yf[c], xf[a], acc[a][c]);
+        }
+        // ---- stage the next K step into the other buffer
+        if (more) {
+            if (XK == MEM) xt.store(Xn, tid, xmode);
+            else gen_tile<T, XK, FAMILY, BM, NT>(p.xg, i0, kn, p.M, p.K, Xn, tid);
+            if (YK == MEM) yt.store(Yn, tid, ymode);
+            else gen_tile<T, YK, FAMILY, BN, NT>(p.yg, j0, kn, p.N, p.K, Yn, tid);
+        }
+        __syncthreads();
+    }
+
+    // ---- epilogue: C = alpha*acc + beta*C (beta == 0: C is not read)
+    T *C = (T *)p.C;
+    const T alpha = (T)p.alpha, beta = (T)p.beta;
+#pragma unroll
+    for (int a = 0; a < FA; ++a) {
+        const int64_t i = i0 + wm * WM + 16 * a + r;
+#pragma unroll
+        for (int c = 0; c < FB; ++c) {
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                const int64_t j = j0 + wn * WN + 16 * c + Mfma<T>::drow(lane, reg);
+                if (i < p.M && j < p.N) {
+                    T *dst = C + i + j * p.ldc;
+                    const T v = alpha * acc[a][c][reg];
+                    *dst = (beta == (T)0) ? v : v + beta * *dst;
+                }
+            }
+        }
+    }
+}
+
+template <typename T>
+__global__ void scale_kernel(int64_t M, int64_t N, T beta, T *C, int64_t ldc) {
+    const int64_t total = M * N;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = e % M, j = e / M;
+        T *c = C + i + j * ldc;
+        *c = (beta == (T)0) ? (T)0 : beta * *c;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Dispatch
+// ------------------------------------------------------------------------------------------
+template <typename T, int XK, int YK, int FAMILY, int BM, int BN, int WMS, int WNS>
+static hipError_t launch_one(const GemmProblem &p, hipStream_t s) {
+    const int64_t nb = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+    if (nb <= 0) return hipSuccess;
+    hipLaunchKernelGGL((skge_gemm_kernel<T, XK, YK, FAMILY, BM, BN, WMS, WNS>), dim3((unsigned)nb),
+                       dim3(64 * WMS * WNS), 0, s, p);
+    return hipGetLastError();
+}
+
+template <typename T>
+static hipError_t launch_gemm(const GemmProblem &p, hipStream_t s) {
+    const bool unif = (p.xkind != MEM ? p.xg.family : p.yg.family) == rb::UNIFORM;
+#define RBH_FAM(XK, YK, BM, BN, WMS, WNS)                                                    \
+    return unif ? launch_one<T, XK, YK, rb::UNIFORM, BM, BN, WMS, WNS>(p, s)                  \
+                : launch_one<T, XK, YK, rb::GAUSSIAN, BM, BN, WMS, WNS>(p, s)
+    if (p.xkind == GEN_OK && p.ykind == MEM) { RBH_FAM(GEN_OK, MEM, 128, 256, 2, 4); }
+    if (p.xkind == GEN_OO && p.ykind == MEM) { RBH_FAM(GEN_OO, MEM, 128, 256, 2, 4); }
+    if (p.xkind == MEM && p.ykind == GEN_OK) { RBH_FAM(MEM, GEN_OK, 256, 128, 4, 2); }
+    if (p.xkind == MEM && p.ykind == GEN_OO) { RBH_FAM(MEM, GEN_OO, 256, 128, 4, 2); }
+#undef RBH_FAM
+    if (p.xkind == MEM && p.ykind == MEM) return launch_one<T, MEM, MEM, rb::GAUSSIAN, 128, 256, 2, 4>(p, s);
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_gemm_f64(const GemmProblem &p, hipStream_t s) { return launch_gemm<double>(p, s); }
+hipError_t launch_gemm_f32(const GemmProblem &p, hipStream_t s) { return launch_gemm<float>(p, s); }
+
+template <typename T>
+static hipError_t launch_scale(int64_t M, int64_t N, T beta, T *C, int64_t ldc, hipStream_t s) {
+    if (M <= 0 || N <= 0) return hipSuccess;
+    int64_t blocks = (M * N + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(scale_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, s, M, N, beta, C, ldc);
+    return hipGetLastError();
+}
+hipError_t launch_scale_f64(int64_t M, int64_t N, double beta, double *C, int64_t ldc, hipStream_t s) {
+    return launch_scale<double>(M, N, beta, C, ldc, s);
+}
+hipError_t launch_scale_f32(int64_t M, int64_t N, float beta, float *C, int64_t ldc, hipStream_t s) {
+    return launch_scale<float>(M, N, beta, C, ldc, s);
+}
+
+}  // namespace rbh

@@ -1,0 +1,109 @@
+"""CPU tests of the C ABI library: it loads, exports every declared symbol, and its host-only logic
+(RNG state bookkeeping, argument checks with the reference's error messages) matches the oracle.
+No GPU work is issued here."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import randblas_amd as rb
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    with open(os.path.join(ROOT, "include", "randblas_hip.h")) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"\b(rbh_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    syms = declared_symbols()
+    assert len(syms) >= 19
+    missing = [s for s in syms if not hasattr(rb.lib, s)]
+    assert not missing, f"missing exports: {missing}"
+
+
+def test_abi_version():
+    assert rb.abi_version() == 1
+
+
+@pytest.mark.parametrize("dims", [(10, 37), (37, 10), (64, 64), (5, 3), (1024, 16384)])
+@pytest.mark.parametrize("major", ["L", "S"])
+def test_dense_next_state_matches_oracle(dims, major):
+    R, C = dims
+    got = rb.dense_next_state(rb.DenseDist(R, C, "G", major), rb.RNGState(key=1, counter=(7, 0, 0, 0)))
+    assert list(got.counter) == O.dense_next_state(R, C, major, counter=(7, 0, 0, 0))
+    assert got.key == 1
+
+
+def test_dense_next_state_carry():
+    got = rb.dense_next_state(rb.DenseDist(4096, 4096), rb.RNGState(key=0, counter=(2**32 - 5, 2**32 - 1, 0, 0)))
+    assert list(got.counter) == O.dense_next_state(4096, 4096, "L", counter=(2**32 - 5, 2**32 - 1, 0, 0))
+
+
+@pytest.mark.parametrize("major", ["S", "L"])
+def test_sparse_next_state_and_nnz(major):
+    D = rb.SparseDist(19, 201, 3, major)
+    assert list(rb.sparse_next_state(D, rb.RNGState(0)).counter) == O.sparse_next_state(19, 201, 3, major)
+    assert D.nnz == O.sparse_nnz(19, 201, 3, major)
+
+
+def _expect_require(fn, *args, fragment):
+    with pytest.raises(rb.RandBLASError) as ei:
+        fn(*args)
+    assert ei.value.code == rb.RBH_ERR_REQUIRE
+    msg = str(ei.value)
+    assert "was required, but did not hold, in function" in msg
+    assert fragment in msg
+
+
+def test_argument_checks_dense():
+    """The reference's randblas_require conditions (skge.hh:197-206, 346-355) and message format."""
+    S = rb.DenseSkOp(rb.DenseDist(10, 50), rb.RNGState(0))
+    A = np.zeros(50 * 8)
+    B = np.zeros(10 * 8)
+    _expect_require(rb.sketch_general_left, "C", "N", "N", 10, 8, 50, 1.0, S, A, 50, 0.0, B, 9,
+                    fragment="ldb >= d")
+    _expect_require(rb.sketch_general_left, "C", "N", "N", 10, 8, 50, 1.0, S, A, 49, 0.0, B, 10,
+                    fragment="lda >= rows_A")
+    _expect_require(rb.sketch_general_left, "C", "N", "N", 10, 8, 50, 1.0, S, A, 50, 0.0, B, 10, 1, 0,
+                    fragment="D->n_rows >= rows_submat_S + ro_s")
+    _expect_require(rb.sketch_general_left, "R", "N", "N", 10, 8, 50, 1.0, S, A, 7, 0.0, B, 8,
+                    fragment="lda >= cols_A")
+    St = rb.DenseSkOp(rb.DenseDist(50, 10), rb.RNGState(0))
+    _expect_require(rb.sketch_general_right, "C", "N", "N", 8, 10, 50, 1.0, A, 8, St, 0.0, B, 7,
+                    fragment="ldb >= m")
+    bb = rb.DenseSkOp(rb.DenseDist(10, 50, "B"), rb.RNGState(0))
+    _expect_require(rb.sketch_general_left, "C", "N", "N", 10, 8, 50, 1.0, bb, A, 50, 0.0, B, 10,
+                    fragment="D->family != 'B'")
+
+
+def test_argument_checks_sparse():
+    S = rb.SparseSkOp(rb.SparseDist(10, 50, 3), rb.RNGState(0))
+    A = np.zeros(50 * 8)
+    B = np.zeros(10 * 8)
+    _expect_require(rb.sketch_general_left, "C", "N", "N", 11, 8, 50, 1.0, S, A, 50, 0.0, B, 11,
+                    fragment="A_rows >= d")
+    _expect_require(rb.sketch_general_left, "C", "N", "N", 10, 8, 50, 1.0, S, A, 50, 0.0, B, 9,
+                    fragment="ldc >= d")
+    bad = rb.SparseSkOp(rb.SparseDist(10, 50, 11), rb.RNGState(0))
+    with pytest.raises(rb.RandBLASError) as ei:
+        rb.sketch_general_left("C", "N", "N", 10, 8, 50, 1.0, bad, A, 50, 0.0, B, 10)
+    assert "vec_nnz > dim_major" in str(ei.value)
+
+
+def test_argument_checks_fill_dense():
+    buf = np.zeros(100)
+    with pytest.raises(rb.RandBLASError) as ei:
+        rb.fill_dense("C", rb.DenseDist(10, 10), 10, 10, 1, 0, buf, rb.RNGState(0))
+    assert "D->n_rows >= n_rows + ro_s" in str(ei.value)
+
+
+def test_header_structs_match_ctypes():
+    assert ctypes.sizeof(rb.RNGStateC) == 24
+    assert ctypes.sizeof(rb.DenseDistC) == 24
+    assert ctypes.sizeof(rb.SparseDistC) == 32

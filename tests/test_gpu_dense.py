@@ -1,0 +1,266 @@
+"""GPU parity tests: dense sketching (fill_dense, sketch_general with a DenseSkOp) through the C ABI.
+
+Oracle: tests/oracle_lib.py (CPU restatement of the reference). Criteria:
+  * operator samples: bitwise equal to the oracle (the reference's own fill_dense output);
+  * sketches: |B_gpu - B_ref| <= E elementwise with the reference's componentwise bound
+    E = (|alpha| m 2 eps) |op(S)| |op(A)| + |beta| eps |B0|   (test/test_matmul_cores/linop_common.hh:257-263);
+  * identity probes: approx_equal with atol = 10 eps, rtol = eps (test/comparison.hh:59-82).
+Cases follow test/test_matmul_cores/test_lskge3.cc:121-306 and test_rskge3.cc.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle_lib as O
+import randblas_amd as rb
+
+pytestmark = pytest.mark.gpu
+
+DT = {np.float64: torch.float64, np.float32: torch.float32}
+
+
+def dev(x, cuda):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(cuda)
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+# --------------------------------------------------------------------------------------------
+# fill_dense: bitwise
+# --------------------------------------------------------------------------------------------
+FILL_CASES = [
+    # (D_rows, D_cols, family, major, n_rows, n_cols, ro, co, layout)
+    (30, 200, "G", "L", 30, 200, 0, 0, "R"),
+    (30, 200, "G", "L", 30, 200, 0, 0, "C"),
+    (200, 30, "G", "L", 200, 30, 0, 0, "C"),
+    (8, 12, "G", "L", 3, 10, 3, 1, "C"),
+    (8, 12, "G", "S", 3, 10, 3, 1, "R"),
+    (12, 8, "U", "L", 10, 3, 1, 3, "R"),
+    (13, 7, "U", "S", 5, 6, 2, 1, "C"),
+    (1000, 2001, "G", "L", 999, 1997, 1, 3, "R"),
+    (2001, 1000, "G", "S", 1500, 900, 7, 5, "C"),
+    (1024, 16384, "G", "L", 64, 16384, 960, 0, "R"),
+]
+
+
+@pytest.mark.parametrize("case", FILL_CASES)
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_fill_dense_bitwise(cuda, case, dtype):
+    R, C, fam, maj, r, c, ro, co, layout = case
+    exp, nxt = O.fill_dense(layout, R, C, fam, maj, r, c, ro, co, key=7, counter=(3, 0, 0, 0), dtype=dtype)
+    buf = torch.empty(r * c, dtype=DT[dtype], device=cuda)
+    D = rb.DenseDist(R, C, fam, maj)
+    got_next = rb.fill_dense(layout, D, r, c, ro, co, buf, rb.RNGState(key=7, counter=(3, 0, 0, 0)))
+    got = host(buf)
+    assert np.array_equal(got.view(np.uint64 if dtype == np.float64 else np.uint32),
+                          exp.view(np.uint64 if dtype == np.float64 else np.uint32)), \
+        f"{np.sum(got != exp)} of {got.size} samples differ"
+    assert list(got_next.counter) == nxt
+
+
+def test_fill_dense_counter_carry(cuda):
+    """Counter near 2^32 and 2^64: the 128-bit add must carry exactly as ctr_type::incr."""
+    for counter in [(0xFFFFFFF0, 0, 0, 0), (0xFFFFFFFF, 0xFFFFFFFF, 5, 0), (1, 2, 3, 4)]:
+        exp, _ = O.fill_dense("R", 40, 400, "G", "L", 40, 400, 0, 0, key=9, counter=counter)
+        buf = torch.empty(40 * 400, dtype=torch.float64, device=cuda)
+        rb.fill_dense("R", rb.DenseDist(40, 400), 40, 400, 0, 0, buf, rb.RNGState(key=9, counter=counter))
+        assert np.array_equal(host(buf), exp)
+
+
+# --------------------------------------------------------------------------------------------
+# sketch_general (left / right) vs oracle within E
+# --------------------------------------------------------------------------------------------
+def _explicit_S(layout, SR, SC, fam, maj, key, dtype):
+    S, _ = O.fill_dense(layout, SR, SC, fam, maj, SR, SC, 0, 0, key=key, dtype=dtype)
+    lds = SR if layout == "C" else SC
+    return S, lds
+
+
+def _pos(layout, lds, ro, co):
+    return ro + co * lds if layout == "C" else ro * lds + co
+
+
+def check_left(cuda, layout, opS, opA, d, n, m, alpha, beta, SR, SC, ro, co, dtype, fam="G", maj="L",
+               explicit=False, skey=0):
+    rA, cA = (m, n) if opA == "N" else (n, m)
+    A = O.random_matrix(rA, cA, 99, dtype)
+    lda = rA if layout == "C" else cA
+    B0 = O.random_matrix(d, n, 42, dtype)
+    ldb = d if layout == "C" else n
+    # reference value (oracle) and bound
+    Bexp = B0.copy()
+    O.lskge3(layout, opS, opA, d, n, m, alpha, SR, SC, fam, maj, skey, ro, co, A, lda, beta, Bexp, ldb)
+    S, lds = _explicit_S(layout, SR, SC, fam, maj, skey, dtype)
+    pos = _pos(layout, lds, ro, co)
+    E = O.error_bound_left(layout, opS, opA, d, n, m, alpha, np.abs(S[pos:]).copy(), lds, A, lda, beta, B0, ldb, dtype)
+    # device
+    Sop = rb.DenseSkOp(rb.DenseDist(SR, SC, fam, maj), rb.RNGState(key=skey))
+    if explicit:
+        Sop.buff = dev(S, cuda)
+        Sop.buff_layout = layout
+    dB = dev(B0, cuda)
+    rb.sketch_general_left(layout, opS, opA, d, n, m, alpha, Sop, dev(A, cuda), lda, beta, dB, ldb, ro_s=ro, co_s=co)
+    got = host(dB)
+    err = np.abs(got - Bexp)
+    assert np.all(err <= E), f"max err/E = {np.max(err / np.maximum(E, np.finfo(dtype).tiny))}"
+    return got
+
+
+LEFT_CASES = [
+    # (d, n, m, SR, SC, ro, co) with op(submat S) d x m
+    (30, 12, 200, 30, 200, 0, 0),       # sketching
+    (51, 12, 10, 51, 10, 0, 0),         # lifting
+    (3, 10, 10, 8, 12, 3, 1),           # submatrix of S (test_lskge3.cc)
+    (130, 260, 300, 140, 320, 5, 17),   # several tiles, ragged edges, unaligned co
+    (256, 512, 1024, 256, 1024, 0, 0),  # full tiles
+]
+
+
+@pytest.mark.parametrize("case", LEFT_CASES)
+@pytest.mark.parametrize("layout", ["C", "R"])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_lskge3_fused(cuda, case, layout, dtype):
+    d, n, m, SR, SC, ro, co = case
+    check_left(cuda, layout, "N", "N", d, n, m, 1.0, 0.0, SR, SC, ro, co, dtype)
+
+
+@pytest.mark.parametrize("opS,opA", [("T", "N"), ("N", "T"), ("T", "T")])
+@pytest.mark.parametrize("layout", ["C", "R"])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_lskge3_ops(cuda, opS, opA, layout, dtype):
+    d, n, m = 37, 45, 150
+    SR, SC = (d + 4, m + 9) if opS == "N" else (m + 4, d + 9)
+    check_left(cuda, layout, opS, opA, d, n, m, 0.5, -1.0, SR, SC, 3, 6, dtype)
+
+
+@pytest.mark.parametrize("fam,maj", [("G", "S"), ("U", "L"), ("U", "S")])
+@pytest.mark.parametrize("layout", ["C", "R"])
+def test_lskge3_families_major_axes(cuda, fam, maj, layout):
+    check_left(cuda, layout, "N", "N", 40, 33, 170, 2.0, 0.0, 50, 180, 4, 5, np.float64, fam=fam, maj=maj)
+    check_left(cuda, layout, "T", "N", 40, 33, 170, 2.0, 0.0, 180, 50, 5, 4, np.float64, fam=fam, maj=maj)
+
+
+@pytest.mark.parametrize("layout", ["C", "R"])
+@pytest.mark.parametrize("opS", ["N", "T"])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_lskge3_explicit_buffer(cuda, layout, opS, dtype):
+    """Preallocated S.buff (fill_dense(S) or BlackBox) goes through the memory-operand GEMM."""
+    d, n, m = 29, 31, 140
+    SR, SC = (d + 2, m + 3) if opS == "N" else (m + 2, d + 3)
+    check_left(cuda, layout, opS, "N", d, n, m, 1.0, 0.5, SR, SC, 1, 2, dtype, explicit=True)
+
+
+def test_lskge3_alpha_zero_beta(cuda):
+    d, n, m = 20, 30, 40
+    B0 = np.random.default_rng(0).standard_normal(d * n)
+    dB = dev(B0, cuda)
+    A = dev(np.full(m * n, np.nan), cuda)   # alpha == 0: A must not be read (BLAS semantics)
+    S = rb.DenseSkOp(rb.DenseDist(d, m), rb.RNGState(0))
+    rb.sketch_general_left("C", "N", "N", d, n, m, 0.0, S, A, m, 2.0, dB, d)
+    assert np.array_equal(host(dB), 2.0 * B0)
+    dB = dev(np.full(d * n, np.nan), cuda)   # beta == 0: B must not be read
+    rb.sketch_general_left("C", "N", "N", d, n, m, 1.0, S, dev(np.ones(m * n), cuda), m, 0.0, dB, d)
+    assert np.all(np.isfinite(host(dB)))
+
+
+def test_lskge3_identity_probe(cuda):
+    """test_left_apply_submatrix_to_eye (linop_common.hh:305-355): B = alpha submat(S) I + beta B."""
+    for layout in "CR":
+        for dtype in (np.float64, np.float32):
+            d0, m0, d1, m1, ro, co = 8, 12, 3, 10, 3, 1
+            alpha, beta = 2.5, -0.5
+            A = np.eye(m1, dtype=dtype).ravel()
+            B0 = O.random_matrix(d1, m1, 42, dtype)
+            ldb = d1 if layout == "C" else m1
+            S, lds = _explicit_S(layout, d0, m0, "G", "L", 0, dtype)
+            S2 = S.reshape((d0, m0), order="F" if layout == "C" else "C")
+            Bm = B0.reshape((d1, m1), order="F" if layout == "C" else "C")
+            exp = alpha * S2[ro:ro + d1, co:co + m1] + beta * Bm
+            dB = dev(B0, cuda)
+            rb.sketch_general_left(layout, "N", "N", d1, m1, m1, dtype(alpha),
+                                   rb.DenseSkOp(rb.DenseDist(d0, m0), rb.RNGState(0)), dev(A, cuda), m1,
+                                   dtype(beta), dB, ldb, ro_s=ro, co_s=co)
+            got = host(dB).reshape((d1, m1), order="F" if layout == "C" else "C")
+            eps = np.finfo(dtype).eps
+            diff = np.abs(got - exp)
+            ok = (diff <= 10 * eps) | (diff <= np.maximum(np.abs(got), np.abs(exp)) * eps)
+            assert np.all(ok)
+
+
+def check_right(cuda, layout, opA, opS, m, d, n, alpha, beta, SR, SC, ro, co, dtype, fam="G", maj="L",
+                explicit=False, skey=0):
+    rA, cA = (m, n) if opA == "N" else (n, m)
+    A = O.random_matrix(rA, cA, 57, dtype)
+    lda = rA if layout == "C" else cA
+    B0 = O.random_matrix(m, d, 10, dtype)
+    ldb = m if layout == "C" else d
+    Bexp = B0.copy()
+    O.rskge3(layout, opA, opS, m, d, n, alpha, A, lda, SR, SC, fam, maj, skey, ro, co, beta, Bexp, ldb)
+    S, lds = _explicit_S(layout, SR, SC, fam, maj, skey, dtype)
+    pos = _pos(layout, lds, ro, co)
+    eps = np.finfo(dtype).eps
+    E = np.abs(B0).astype(dtype) if beta != 0 else np.zeros_like(B0)
+    O.gemm(layout, opA, opS, m, d, n, abs(alpha) * n * 2 * eps, np.abs(A), lda, np.abs(S[pos:]).copy(), lds,
+           abs(beta) * eps, E, ldb)
+    Sop = rb.DenseSkOp(rb.DenseDist(SR, SC, fam, maj), rb.RNGState(key=skey))
+    if explicit:
+        Sop.buff = dev(S, cuda)
+        Sop.buff_layout = layout
+    dB = dev(B0, cuda)
+    rb.sketch_general_right(layout, opA, opS, m, d, n, alpha, dev(A, cuda), lda, Sop, beta, dB, ldb, ro_s=ro, co_s=co)
+    got = host(dB)
+    err = np.abs(got - Bexp)
+    assert np.all(err <= E), f"max err/E = {np.max(err / np.maximum(E, np.finfo(dtype).tiny))}"
+
+
+RIGHT_CASES = [
+    # (m, d, n, SR, SC, ro, co): op(submat S) is n x d
+    (12, 30, 200, 200, 30, 0, 0),
+    (12, 51, 10, 10, 51, 0, 0),
+    (10, 3, 10, 12, 8, 1, 3),
+    (260, 130, 300, 320, 140, 17, 5),
+    (512, 256, 1024, 1024, 256, 0, 0),
+]
+
+
+@pytest.mark.parametrize("case", RIGHT_CASES)
+@pytest.mark.parametrize("layout", ["C", "R"])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_rskge3_fused(cuda, case, layout, dtype):
+    m, d, n, SR, SC, ro, co = case
+    check_right(cuda, layout, "N", "N", m, d, n, 1.0, 0.0, SR, SC, ro, co, dtype)
+
+
+@pytest.mark.parametrize("opA,opS", [("T", "N"), ("N", "T"), ("T", "T")])
+@pytest.mark.parametrize("layout", ["C", "R"])
+def test_rskge3_ops(cuda, opA, opS, layout):
+    m, d, n = 45, 37, 150
+    SR, SC = (n + 4, d + 9) if opS == "N" else (d + 4, n + 9)
+    check_right(cuda, layout, opA, opS, m, d, n, 0.5, -1.0, SR, SC, 3, 6, np.float64)
+    check_right(cuda, layout, opA, opS, m, d, n, 0.5, -1.0, SR, SC, 3, 6, np.float64, explicit=True)
+
+
+def test_lskge3_large_c2_slice(cuda):
+    """BASELINE config 2 shape family at reduced n (d=1024, m=16384): fused vs oracle within E."""
+    d, n, m = 1024, 256, 16384
+    check_left(cuda, "C", "N", "N", d, n, m, 1.0, 0.0, d, m, 0, 0, np.float64)
+
+
+def test_row_shards_reassemble(cuda):
+    """Output-row sharding (§8(e)): the union of ro_s-offset shards is bitwise the unsharded sketch."""
+    d, n, m = 512, 300, 2048
+    A = dev(O.random_matrix(m, n, 99), cuda)
+    S = rb.DenseSkOp(rb.DenseDist(d, m), rb.RNGState(0))
+    full = torch.empty(d * n, dtype=torch.float64, device=cuda)
+    rb.sketch_general_left("C", "N", "N", d, n, m, 1.0, S, A, m, 0.0, full, d)
+    full = host(full).reshape((d, n), order="F")
+    G = 4
+    parts = []
+    for g in range(G):
+        part = torch.empty((d // G) * n, dtype=torch.float64, device=cuda)
+        rb.sketch_general_left("C", "N", "N", d // G, n, m, 1.0, S, A, m, 0.0, part, d // G, ro_s=g * d // G)
+        parts.append(host(part).reshape((d // G, n), order="F"))
+    assert np.array_equal(np.vstack(parts), full)

@@ -1,0 +1,140 @@
+"""GPU parity tests: sparse sketching operators (SASO / LASO) through the C ABI.
+
+Oracle: tests/oracle_lib.py. Criteria:
+  * fill_sparse: (rows, cols, vals) bitwise equal to the reference's repeated_fisher_yates output;
+  * sketch_general with a SparseSkOp: bitwise equal to the reference's left_spmm COO path, which
+    accumulates each output in ascending contracted index with separate multiply and add
+    (csc_spmm_impl.hh:43-65); the device kernel keeps that order, so no tolerance is needed.
+Cases follow test/test_matmul_cores/test_lskges.cc:174-589 and test_rskges.cc: keys {42, 0, 1},
+vec_nnz {1, 2, 3, 7, 19}, sketching 19 x 201 and lifting 201 x 19 with n = 12, submatrices,
+transposes, alpha = 5.5, beta in {0, -1}.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle_lib as O
+import randblas_amd as rb
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(x, cuda):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(cuda)
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def bits(x):
+    return x.view(np.uint64 if x.dtype == np.float64 else np.uint32)
+
+
+@pytest.mark.parametrize("dims", [(19, 201), (201, 19), (1024, 16384), (300, 300)])
+@pytest.mark.parametrize("vec_nnz", [1, 2, 3, 7, 19])
+@pytest.mark.parametrize("major", ["S", "L"])
+@pytest.mark.parametrize("key", [42, 0, 1])
+def test_fill_sparse_bitwise(cuda, dims, vec_nnz, major, key):
+    R, C = dims
+    if vec_nnz > (min(R, C) if major == "S" else max(R, C)):
+        pytest.skip("vec_nnz > dim_major")
+    rows, cols, vals = O.fill_sparse(R, C, vec_nnz, major, key=key)
+    nnz = len(rows)
+    dr = torch.empty(nnz, dtype=torch.int64, device=cuda)
+    dc = torch.empty(nnz, dtype=torch.int64, device=cuda)
+    dv = torch.empty(nnz, dtype=torch.float64, device=cuda)
+    S = rb.SparseSkOp(rb.SparseDist(R, C, vec_nnz, major), rb.RNGState(key=key))
+    rb.fill_sparse(S, dr, dc, dv)
+    assert np.array_equal(host(dr), rows)
+    assert np.array_equal(host(dc), cols)
+    assert np.array_equal(host(dv), vals)
+
+
+def check_left(cuda, layout, opS, opA, d, n, m, alpha, beta, SR, SC, vec, major, key, ro, co, dtype, given=False):
+    rA, cA = (m, n) if opA == "N" else (n, m)
+    A = O.random_matrix(rA, cA, 99, dtype)
+    lda = rA if layout == "C" else cA
+    B0 = O.random_matrix(d, n, 42, dtype)
+    ldb = d if layout == "C" else n
+    rows, cols, vals = O.fill_sparse(SR, SC, vec, major, key=key, dtype=dtype)
+    Bexp = B0.copy()
+    O.left_spmm_coo(layout, opS, opA, d, n, m, alpha, SR, SC, rows, cols, vals, ro, co, A, lda, beta, Bexp, ldb)
+    S = rb.SparseSkOp(rb.SparseDist(SR, SC, vec, major), rb.RNGState(key=key))
+    if given:   # user-provided COO arrays (SparseSkOp(dist, state, rows, cols, vals), sparse_skops.hh:268-291)
+        perm = np.random.default_rng(5).permutation(len(rows))
+        S.rows, S.cols, S.vals = dev(rows[perm], cuda), dev(cols[perm], cuda), dev(vals[perm], cuda)
+        S.nnz = len(rows)
+    dB = dev(B0, cuda)
+    rb.sketch_general_left(layout, opS, opA, d, n, m, alpha, S, dev(A, cuda), lda, beta, dB, ldb, ro_s=ro, co_s=co)
+    got = host(dB)
+    assert np.array_equal(bits(got), bits(Bexp)), f"{np.sum(got != Bexp)} of {got.size} entries differ"
+
+
+@pytest.mark.parametrize("vec_nnz", [1, 2, 3, 7, 19])
+@pytest.mark.parametrize("key", [42, 0, 1])
+@pytest.mark.parametrize("layout", ["C", "R"])
+def test_lskges_sketch_and_lift(cuda, vec_nnz, key, layout):
+    # sketching: S is 19 x 201 (SASO), B = S A with A 201 x 12
+    check_left(cuda, layout, "N", "N", 19, 12, 201, 1.0, 0.0, 19, 201, vec_nnz, "S", key, 0, 0, np.float64)
+    # lifting: S is 201 x 19, B = S A with A 19 x 12
+    if vec_nnz <= 19:
+        check_left(cuda, layout, "N", "N", 201, 12, 19, 1.0, 0.0, 201, 19, vec_nnz, "S", key, 0, 0, np.float64)
+
+
+@pytest.mark.parametrize("major", ["S", "L"])
+@pytest.mark.parametrize("opS,opA", [("N", "N"), ("T", "N"), ("N", "T"), ("T", "T")])
+@pytest.mark.parametrize("layout", ["C", "R"])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_lskges_submatrix_ops(cuda, major, opS, opA, layout, dtype):
+    d, n, m = 10, 12, 150
+    SR, SC = (19, 201) if opS == "N" else (201, 19)
+    ro, co = (3, 20) if opS == "N" else (20, 3)
+    check_left(cuda, layout, opS, opA, d, n, m, 5.5, -1.0, SR, SC, 3, major, 42, ro, co, dtype)
+
+
+@pytest.mark.parametrize("layout", ["C", "R"])
+def test_lskges_user_coo(cuda, layout):
+    check_left(cuda, layout, "N", "N", 19, 12, 201, 0.5, -1.0, 19, 201, 7, "S", 0, 0, 0, np.float64, given=True)
+    check_left(cuda, layout, "T", "N", 19, 12, 201, 0.5, 0.0, 201, 19, 7, "S", 0, 0, 0, np.float64, given=True)
+
+
+def test_lskges_config3_slice(cuda):
+    """BASELINE config 3 operator (SASO d=1024, m=16384, vec_nnz=8) on a 64-column slice of A."""
+    check_left(cuda, "C", "N", "N", 1024, 64, 16384, 1.0, 0.0, 1024, 16384, 8, "S", 0, 0, 0, np.float64)
+
+
+def check_right(cuda, layout, opA, opS, m, d, n, alpha, beta, SR, SC, vec, major, key, ro, co, dtype):
+    rA, cA = (m, n) if opA == "N" else (n, m)
+    A = O.random_matrix(rA, cA, 57, dtype)
+    lda = rA if layout == "C" else cA
+    B0 = O.random_matrix(m, d, 10, dtype)
+    ldb = m if layout == "C" else d
+    rows, cols, vals = O.fill_sparse(SR, SC, vec, major, key=key, dtype=dtype)
+    Bexp = B0.copy()
+    O.right_spmm_coo(layout, opA, opS, m, d, n, alpha, A, lda, SR, SC, rows, cols, vals, ro, co, beta, Bexp, ldb)
+    S = rb.SparseSkOp(rb.SparseDist(SR, SC, vec, major), rb.RNGState(key=key))
+    dB = dev(B0, cuda)
+    rb.sketch_general_right(layout, opA, opS, m, d, n, alpha, dev(A, cuda), lda, S, beta, dB, ldb, ro_s=ro, co_s=co)
+    got = host(dB)
+    assert np.array_equal(bits(got), bits(Bexp)), f"{np.sum(got != Bexp)} of {got.size} entries differ"
+
+
+@pytest.mark.parametrize("major", ["S", "L"])
+@pytest.mark.parametrize("opA,opS", [("N", "N"), ("T", "N"), ("N", "T"), ("T", "T")])
+@pytest.mark.parametrize("layout", ["C", "R"])
+def test_rskges(cuda, major, opA, opS, layout):
+    m, d, n = 12, 10, 150
+    SR, SC = (201, 19) if opS == "N" else (19, 201)
+    ro, co = (20, 3) if opS == "N" else (3, 20)
+    check_right(cuda, layout, opA, opS, m, d, n, 5.5, -1.0, SR, SC, 3, major, 1, ro, co, np.float64)
+    check_right(cuda, layout, opA, opS, m, d, n, 1.0, 0.0, SR, SC, 3, major, 1, ro, co, np.float32)
+
+
+def test_lskges_alpha_zero(cuda):
+    B0 = np.random.default_rng(0).standard_normal(19 * 12)
+    dB = dev(B0, cuda)
+    S = rb.SparseSkOp(rb.SparseDist(19, 201, 3), rb.RNGState(0))
+    rb.sketch_general_left("C", "N", "N", 19, 12, 201, 0.0, S, dev(np.ones(201 * 12), cuda), 201, -1.0, dB, 19)
+    assert np.array_equal(host(dB), -B0)
