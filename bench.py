@@ -18,6 +18,7 @@ reference's algorithm, oracle/) on a bounded column sample, rank 0 only.
 from __future__ import annotations
 
 import argparse
+import faulthandler
 import json
 import os
 import sys
@@ -54,7 +55,10 @@ def cpu_baseline(kind, dtype, d, m, n, vec_nnz, target_s=10.0):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
 
-    cores = os.cpu_count() or 1
+    # threads actually used: the box's CPU share (OMP_NUM_THREADS) rather than every core the
+    # machine reports (os.cpu_count() is many times the share on the GPU box)
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    cores = max(1, min(cores, os.cpu_count() or 1))
     O.set_threads(cores)
     npdt = np.float64 if dtype == "f64" else np.float32
 
@@ -90,6 +94,7 @@ def cpu_baseline(kind, dtype, d, m, n, vec_nnz, target_s=10.0):
 
 
 def main():
+    faulthandler.enable()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)

@@ -22,6 +22,14 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "librandblas_hip.so")
 
+# One HIP runtime per process: torch ships its own libamdhip64 (soname libamdhip64.so.7). Loading
+# torch first makes this library bind to that same runtime instead of /opt/rocm's copy, so device
+# pointers from torch tensors are valid here and vice versa.
+try:
+    import torch  # noqa: F401
+except ImportError:  # pragma: no cover - torch is optional for host-pointer use
+    torch = None
+
 if not os.path.exists(LIB_PATH):
     raise ImportError(
         f"randblas_amd: {LIB_PATH} is missing; build it with `python -c 'import __graft_entry__ as g; g.build()'`"

@@ -39,8 +39,8 @@ __global__ void fill_sparse_kernel(uint32_t c0, uint32_t c1, uint32_t c2, uint32
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= dim_minor) return;
     const uint32_t base[4] = {c0, c1, c2, c3};
-    int64_t pos[MAXNNZ];   // positions touched so far (work[pos[t]] = val[t])
-    int64_t val[MAXNNZ];
+    int64_t pos[2 * MAXNNZ];   // positions touched so far (work[pos[t]] = val[t]); <= 2 per draw
+    int64_t val[2 * MAXNNZ];
     int ntouched = 0;
     const int64_t offset = i * vec_nnz;
     for (int64_t j = 0; j < vec_nnz; ++j) {
@@ -230,7 +230,12 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
     int64_t *rowptr = nullptr;
     int32_t *kidx = nullptr;
     void *tmp = nullptr;
-    err = rocprim::radix_sort_pairs(nullptr, tmp_bytes, k_in, k_out, v_in, v_out, n, 0, 64, s);
+    int end_bit = 1;
+    {
+        const unsigned long long maxkey = (unsigned long long)p.M * (unsigned long long)p.K;
+        while (end_bit < 64 && (1ull << end_bit) <= maxkey) ++end_bit;
+    }
+    err = rocprim::radix_sort_pairs(nullptr, tmp_bytes, k_in, k_out, v_in, v_out, n, 0, (unsigned)end_bit, s);
     if (err != hipSuccess) return err;
     const size_t bytes = 2 * n * sizeof(uint64_t) + 2 * n * sizeof(T) + (size_t)(p.M + 1) * sizeof(int64_t) +
                          n * sizeof(int32_t) + tmp_bytes + 256;
@@ -250,12 +255,9 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
     if (nnz > 0) {
         hipLaunchKernelGGL(coo_keys_kernel<T>, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, rows, cols,
                            vals, p.ro, p.co, p.win_r, p.win_c, p.transposed, p.K, (T)p.alpha, k_in, v_in);
-        int end_bit = 1;
-        const unsigned long long maxkey = (unsigned long long)p.M * (unsigned long long)p.K;
-        while (end_bit < 64 && (1ull << end_bit) <= maxkey) ++end_bit;
         // invalid keys (~0) must still sort last: with end_bit < 64 their low bits are all ones,
         // which is >= any valid key below 2^end_bit.
-        err = rocprim::radix_sort_pairs(tmp, tmp_bytes, k_in, k_out, v_in, v_out, (size_t)nnz, 0, end_bit, s);
+        err = rocprim::radix_sort_pairs(tmp, tmp_bytes, k_in, k_out, v_in, v_out, (size_t)nnz, 0, (unsigned)end_bit, s);
         if (err != hipSuccess) { (void)hipFreeAsync(ws, s); return err; }
     }
     hipLaunchKernelGGL(rowptr_kernel, dim3((unsigned)((nnz + 1 + 255) / 256)), dim3(256), 0, s, nnz, k_out, p.M,
