@@ -41,7 +41,7 @@ CONFIGS = {
     "c2": ("dense", "f64", 1024, 16384, 16384, 0),
     "ns": ("dense", "f64", 2048, 16384, 16384, 0),
     "c3": ("saso", "f64", 1024, 16384, 16384, 8),
-    "c4": ("dense", "f32", 2048, 32768, 32768, 0),
+    "c4": ("dense", "f32", 256, 32768, 32768, 0),    # per GPU: d = 2048 at N = 8 (configs[3])
     "c5": ("sksy", "f64", 512, 16384, 16384, 0),
 }
 
@@ -101,6 +101,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--chunks", type=int, default=4, help="column chunks pipelined with the all-gather (N > 1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -119,9 +120,6 @@ def main():
     # A ~ DenseDist(m, n) Gaussian key 99, ColMajor, generated on the device (input, not timed)
     A = torch.empty(m * n, dtype=tdt, device=dev)
     rb.fill_dense("C", rb.DenseDist(m, n), m, n, 0, 0, A, rb.RNGState(99))
-    B = torch.empty(d * n, dtype=tdt, device=dev)
-    full = torch.empty(world * d * n, dtype=tdt, device=dev) if world > 1 else None
-    gathered = torch.empty(world * d * n, dtype=tdt, device=dev) if world > 1 else None
     if kind == "saso":
         S = rb.SparseSkOp(rb.SparseDist(world * d, m, vec_nnz), rb.RNGState(0))
     else:
@@ -130,25 +128,40 @@ def main():
         Am = A.view(n, m)
         A.copy_(((Am + Am.t()) * 0.5).reshape(-1))
 
-    k_ev = []
+    k_ev = []   # (start, end) HIP events around every library call of the timed steps
 
-    def step(record=False):
+    def compute(ro_s, j0, j1, out, record=False):
+        """This rank's shard B[ro_s : ro_s + d, j0 : j1] = S[ro_s : ro_s + d, :] * A[:, j0 : j1]."""
         e0 = e1 = None
         if record:
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)
+        Ach = A[j0 * m:]
         if kind == "sksy":
-            rb.sketch_symmetric_left("C", d, n, 1.0, S, A, m, 0.0, B, d, ro_s=rank * d, sym_check_tol=-1.0)
+            rb.sketch_symmetric_left("C", d, j1 - j0, 1.0, S, Ach, m, 0.0, out, d, ro_s=ro_s, sym_check_tol=-1.0)
         else:
-            rb.sketch_general_left("C", "N", "N", d, n, m, 1.0, S, A, m, 0.0, B, d, ro_s=rank * d)
+            rb.sketch_general_left("C", "N", "N", d, j1 - j0, m, 1.0, S, Ach, m, 0.0, out, d, ro_s=ro_s)
         if record:
             e1.record(stream)
             k_ev.append((e0, e1))
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, B)
-            # [world][n][d] (each shard ColMajor d x n) -> ColMajor (world*d) x n
-            full.view(n, world * d).copy_(gathered.view(world, n, d).permute(1, 0, 2).reshape(n, world * d))
+
+    recording = [False]
+    if world > 1:
+        from randblas_amd.distributed import RowShardedSketch
+
+        B_full = torch.empty(world * d * n, dtype=tdt, device=dev)
+        drv = RowShardedSketch(world * d, n, lambda ro, j0, j1, out: compute(ro, j0, j1, out, recording[0]),
+                               tdt, dev, chunks=args.chunks)
+
+        def step(record=False):
+            recording[0] = record
+            drv(B_full)
+    else:
+        B = torch.empty(d * n, dtype=tdt, device=dev)
+
+        def step(record=False):
+            compute(0, 0, n, B, record)
 
     for _ in range(args.warmup):
         step()
@@ -156,6 +169,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    rb.kernel_timing(True)   # HIP events around each call's dominant kernel, on its launch stream
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(record=True)
@@ -168,17 +182,23 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in k_ev]))
+    call_ms = float(np.sum([a.elapsed_time(b) for a, b in k_ev])) / args.steps   # library time per step
+    kt = rb.kernel_times_ms()
+    rb.kernel_timing(False)
+    launches = len(kt)
+    kern_ms = float(np.mean(kt))            # average duration of one dominant-kernel launch
     ms_step = elapsed * 1e3 / args.steps
+    cols_per_launch = n * args.steps / max(launches, 1)
 
-    # roofline of the dominant kernel
+    # roofline of the dominant kernel: algorithmic work of one launch / its average duration
+    esz = 8 if dtype == "f64" else 4
     if kind == "saso":
-        alg = m * n * (8 if dtype == "f64" else 4) + d * n * (8 if dtype == "f64" else 4)
+        alg = (m * cols_per_launch + d * cols_per_launch) * esz   # read A panel once, write B once
         achieved = alg / (kern_ms * 1e-3)
         roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK, "traffic": None}
     else:
-        flops = 2.0 * d * m * n
+        flops = 2.0 * d * m * cols_per_launch
         achieved = flops / (kern_ms * 1e-3)
         roof = {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK[dtype] / 1e12, "unit": "TFLOP/s",
                 "frac": achieved / PEAK[dtype], "traffic": None}
@@ -200,6 +220,8 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_step,
             "kernel_ms": kern_ms,
+            "kernel_launches_per_step": launches / args.steps,
+            "library_ms_per_step": call_ms,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

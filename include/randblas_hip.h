@@ -56,6 +56,12 @@ typedef struct rbh_sparse_dist {
 int rbh_abi_version(void);
 const char *rbh_last_error(void);
 
+/* Diagnostics (no reference counterpart): HIP-event timing of the dominant kernel of every call
+ * (the fused GEMM, the sparse apply), recorded on the call's stream while enabled. collect()
+ * waits for the recorded kernels, writes up to `max` durations in milliseconds and resets. */
+void rbh_kernel_timing_enable(int on);
+int rbh_kernel_timing_collect(float *ms, int max);
+
 /* ---- RNG state bookkeeping --------------------------------------------------------------- */
 /* dense::compute_next_state (dense_skops.hh:172-191). */
 int rbh_dense_next_state(const rbh_dense_dist *D, const rbh_state *seed, rbh_state *next);

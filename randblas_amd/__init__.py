@@ -74,6 +74,8 @@ def _check(rc: int) -> None:
 P = ctypes.POINTER
 lib.rbh_last_error.restype = ctypes.c_char_p
 lib.rbh_abi_version.restype = ctypes.c_int
+lib.rbh_kernel_timing_enable.argtypes = [ctypes.c_int]
+lib.rbh_kernel_timing_collect.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_int]
 lib.rbh_sparse_nnz.restype = c_i64
 lib.rbh_sparse_nnz.argtypes = [P(SparseDistC)]
 lib.rbh_dense_next_state.argtypes = [P(DenseDistC), P(RNGStateC), P(RNGStateC)]
@@ -345,6 +347,18 @@ def sketch_general(layout, op1, op2, d_or_m, n_or_d, m_or_n, alpha, X, Y, lda_or
     return sketch_general_right(layout, op1, op2, d_or_m, n_or_d, m_or_n, alpha, X, Y, lda_or_none, *args, **kw)
 
 
+def kernel_timing(on: bool) -> None:
+    """Enable/disable HIP-event timing of each call's dominant kernel (diagnostics)."""
+    lib.rbh_kernel_timing_enable(1 if on else 0)
+
+
+def kernel_times_ms(max_n: int = 65536) -> list:
+    """Durations (ms) of the dominant kernels recorded since timing was enabled; resets the record."""
+    buf = (ctypes.c_float * max_n)()
+    k = lib.rbh_kernel_timing_collect(buf, max_n)
+    return [float(buf[i]) for i in range(k)]
+
+
 def abi_version() -> int:
     return int(lib.rbh_abi_version())
 
@@ -353,5 +367,5 @@ __all__ = [
     "RNGState", "DenseDist", "SparseDist", "DenseSkOp", "SparseSkOp", "RandBLASError", "fill_dense", "fill_sparse",
     "sketch_general", "sketch_general_left", "sketch_general_right", "sketch_symmetric_left",
     "sketch_symmetric_right", "require_symmetric", "dense_next_state", "sparse_next_state", "abi_version", "lib",
-    "LIB_PATH",
+    "LIB_PATH", "kernel_timing", "kernel_times_ms",
 ]

@@ -22,6 +22,38 @@
 
 using namespace rbh;
 
+// ---------------------------------------------------------------------------------------------
+// kernel timing hook
+// ---------------------------------------------------------------------------------------------
+namespace {
+struct KernelTiming {
+    bool enabled = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+    size_t used = 0;
+    hipEvent_t pending = nullptr;
+};
+KernelTiming g_timing;
+}  // namespace
+
+namespace rbh {
+void timing_begin(hipStream_t s) {
+    if (!g_timing.enabled) return;
+    if (g_timing.used == g_timing.ev.size()) {
+        hipEvent_t a, b;
+        if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
+        g_timing.ev.emplace_back(a, b);
+    }
+    (void)hipEventRecord(g_timing.ev[g_timing.used].first, s);
+    g_timing.pending = g_timing.ev[g_timing.used].second;
+}
+void timing_end(hipStream_t s) {
+    if (!g_timing.enabled || !g_timing.pending) return;
+    (void)hipEventRecord(g_timing.pending, s);
+    g_timing.pending = nullptr;
+    g_timing.used++;
+}
+}  // namespace rbh
+
 namespace {
 
 thread_local std::string g_last_error;
@@ -628,6 +660,23 @@ int require_symmetric(char layout, const T *A, int64_t n, int64_t lda, T tol, vo
 extern "C" {
 
 int rbh_abi_version(void) { return 1; }
+
+void rbh_kernel_timing_enable(int on) {
+    g_timing.enabled = on != 0;
+    g_timing.used = 0;
+}
+
+int rbh_kernel_timing_collect(float *ms, int max) {
+    int n = 0;
+    for (size_t i = 0; i < g_timing.used && n < max; ++i) {
+        if (hipEventSynchronize(g_timing.ev[i].second) != hipSuccess) break;
+        float t = 0.f;
+        if (hipEventElapsedTime(&t, g_timing.ev[i].first, g_timing.ev[i].second) != hipSuccess) break;
+        ms[n++] = t;
+    }
+    g_timing.used = 0;
+    return n;
+}
 const char *rbh_last_error(void) { return g_last_error.c_str(); }
 
 int rbh_dense_next_state(const rbh_dense_dist *D, const rbh_state *seed, rbh_state *next) {

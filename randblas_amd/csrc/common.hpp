@@ -64,4 +64,9 @@ hipError_t launch_fill_dense_f64(const GenOperand &g, int64_t n_rows_, int64_t n
 hipError_t launch_fill_dense_f32(const GenOperand &g, int64_t n_rows_, int64_t n_cols_, int transpose_out,
                                  float *buff, hipStream_t s);
 
+// Optional HIP-event timing of the dominant kernel of each call (rbh_kernel_timing_* in the C ABI).
+// Launchers bracket their main kernel with these; both are no-ops unless timing is enabled.
+void timing_begin(hipStream_t s);
+void timing_end(hipStream_t s);
+
 }  // namespace rbh

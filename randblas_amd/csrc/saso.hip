@@ -263,6 +263,7 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
     hipLaunchKernelGGL(rowptr_kernel, dim3((unsigned)((nnz + 1 + 255) / 256)), dim3(256), 0, s, nnz, k_out, p.M,
                        p.K, rowptr, kidx);
     const unsigned gx = (unsigned)((p.N + SP_J - 1) / SP_J);
+    timing_begin(s);
     if (p.M <= SP_NT) {
         hipLaunchKernelGGL((saso_apply_kernel<T, 1>), dim3(gx, 1), dim3(SP_NT), 0, s, p, rowptr, kidx, v_out);
     } else {
@@ -270,6 +271,7 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
         hipLaunchKernelGGL((saso_apply_kernel<T, 2>), dim3(gx, gy), dim3(SP_NT), 0, s, p, rowptr, kidx, v_out);
     }
     err = hipGetLastError();
+    timing_end(s);
     hipError_t e2 = hipFreeAsync(ws, s);
     return err != hipSuccess ? err : e2;
 }

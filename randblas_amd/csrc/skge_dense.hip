@@ -308,9 +308,12 @@ template <typename T, int XK, int YK, int FAMILY, int BM, int BN, int WMS, int W
 static hipError_t launch_one(const GemmProblem &p, hipStream_t s) {
     const int64_t nb = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
     if (nb <= 0) return hipSuccess;
+    timing_begin(s);
     hipLaunchKernelGGL((skge_gemm_kernel<T, XK, YK, FAMILY, BM, BN, WMS, WNS>), dim3((unsigned)nb),
                        dim3(64 * WMS * WNS), 0, s, p);
-    return hipGetLastError();
+    hipError_t e = hipGetLastError();
+    timing_end(s);
+    return e;
 }
 
 template <typename T>

@@ -1,0 +1,65 @@
+"""Output-row sharded sketching across the GPUs of a node.
+
+Entry (i, k) of a RandBLAS dense operator is a pure function of (seed, i, k), and a SparseSkOp's
+column k is a pure function of (seed, k) (RandBLAS/dense_skops.hh:109-162,
+RandBLAS/sparse_skops.hh:72-92; the reference's "reproducible submatrices",
+rtd/source/updates/index.rst:34). So rank g of G computes rows [g*d_loc, (g+1)*d_loc) of
+B = S * A by calling sketch_general with ro_s = g*d_loc -- no operator data moves -- and the only
+exchange is the all-gather that reassembles B. That all-gather is pipelined with the compute:
+A's columns are cut into `chunks`; chunk c's shard is all-gathered (RCCL over xGMI on GPU, gloo
+on CPU in tests) while chunk c+1 is computed, then unpacked into the ColMajor d x n result.
+
+The per-shard compute is a callable so the same driver runs the HIP path (bench.py) and the CPU
+oracle (tests/test_distributed_cpu.py):  compute(ro_s, j0, j1, out)  writes the d_loc x (j1-j0)
+ColMajor shard  B[ro_s : ro_s + d_loc, j0 : j1]  into the 1-D tensor `out`.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+class RowShardedSketch:
+    def __init__(self, d_total: int, n: int, compute: Callable[[int, int, int, torch.Tensor], None],
+                 dtype: torch.dtype, device: torch.device, chunks: int = 4, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        if d_total % self.world:
+            raise ValueError(f"d_total={d_total} is not divisible by the world size {self.world}")
+        self.d_total, self.n = d_total, n
+        self.d_loc = d_total // self.world
+        self.compute = compute
+        self.chunks = max(1, min(chunks, n))
+        bounds = [round(i * n / self.chunks) for i in range(self.chunks + 1)]
+        self.cols = [(bounds[i], bounds[i + 1]) for i in range(self.chunks) if bounds[i + 1] > bounds[i]]
+        self.local = [torch.empty(self.d_loc * (j1 - j0), dtype=dtype, device=device) for j0, j1 in self.cols]
+        self.gathered = [torch.empty(self.world * self.d_loc * (j1 - j0), dtype=dtype, device=device)
+                         for j0, j1 in self.cols]
+
+    @property
+    def ro_s(self) -> int:
+        return self.rank * self.d_loc
+
+    def __call__(self, B_full: Optional[torch.Tensor]) -> None:
+        """Compute this rank's shard; if B_full (ColMajor d_total x n, 1-D) is given, reassemble the
+        whole sketch into it on every rank."""
+        works: List = []
+        for c, (j0, j1) in enumerate(self.cols):
+            self.compute(self.ro_s, j0, j1, self.local[c])
+            if self.world > 1 and B_full is not None:
+                works.append(dist.all_gather_into_tensor(self.gathered[c], self.local[c], group=self.group,
+                                                         async_op=True))
+        if B_full is None:
+            return
+        Bv = B_full.view(self.n, self.d_total)   # ColMajor d_total x n == row-major [n][d_total]
+        for c, (j0, j1) in enumerate(self.cols):
+            nc = j1 - j0
+            if self.world > 1:
+                works[c].wait()
+                src = self.gathered[c].view(self.world, nc, self.d_loc).permute(1, 0, 2).reshape(nc, self.d_total)
+            else:
+                src = self.local[c].view(nc, self.d_loc)
+            Bv[j0:j1].copy_(src)
