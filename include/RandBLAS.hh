@@ -1,0 +1,501 @@
+// RandBLAS.hh -- drop-in C++ front end of librandblas_hip.so for the sketch-apply path.
+//
+// A program written against RylieWeaver/RandBLAS (snapshot 2024-10-08) for this path compiles
+// unchanged against this header: it provides the reference's types and overloads
+//   RNGState<r123::Philox4x32> (RandBLAS/base.hh:161-232), MajorAxis (base.hh:138-150),
+//   DenseDistName / DenseDist / DenseSkOp (dense_skops.hh:204-419), fill_dense x3 (:486-592),
+//   SparseDist / SparseSkOp / fill_sparse (sparse_skops.hh:134-413),
+//   sketch_general x8 (skge.hh:771-1214), sketch_symmetric x4 (sksy.hh:165-537),
+//   exceptions::Error (exceptions.hh:45-70), and the blas::Layout / blas::Op enums of BLAS++,
+// and routes every call to the MI355X C ABI (include/randblas_hip.h). Host arrays work as in
+// the reference (they are staged through HBM; the call is synchronous); device arrays
+// (hipMalloc) are used in place. Link with -lrandblas_hip.
+//
+// Dense operators are never materialised: a DenseSkOp whose buff is nullptr is regenerated from
+// its Philox counters inside the fused MFMA GEMM. fill_dense(S) still fills S.buff (host memory,
+// as in the reference), after which the operator is applied from that buffer.
+#pragma once
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+
+#include "randblas_hip.h"
+
+// ---------------------------------------------------------------------------------------------
+// BLAS++ enums used by the API (values chosen to match the C ABI's characters)
+// ---------------------------------------------------------------------------------------------
+namespace blas {
+enum class Layout : char { ColMajor = 'C', RowMajor = 'R' };
+enum class Op : char { NoTrans = 'N', Trans = 'T', ConjTrans = 'C' };
+}  // namespace blas
+
+// ---------------------------------------------------------------------------------------------
+// Random123's Philox4x32 interface as RandBLAS uses it (ctr_type / key_type with incr, operator())
+// ---------------------------------------------------------------------------------------------
+namespace r123 {
+template <int N>
+struct U32Array {
+    using value_type = uint32_t;
+    static constexpr int static_size = N;
+    uint32_t v[N];
+    uint32_t &operator[](int i) { return v[i]; }
+    const uint32_t &operator[](int i) const { return v[i]; }
+    // 128-bit little-endian increment with carry (Random123 array.h incr)
+    U32Array &incr(uint64_t n = 1) {
+        uint64_t carry = n;
+        for (int i = 0; i < N && carry; ++i) {
+            const uint64_t s = (uint64_t)v[i] + (uint32_t)carry;
+            v[i] = (uint32_t)s;
+            carry = (carry >> 32) + (s >> 32);
+        }
+        return *this;
+    }
+    bool operator==(const U32Array &o) const { return std::memcmp(v, o.v, sizeof v) == 0; }
+};
+
+struct Philox4x32 {
+    using ctr_type = U32Array<4>;
+    using key_type = U32Array<2>;
+    ctr_type operator()(ctr_type c, key_type k) const {
+        for (int r = 0; r < 10; ++r) {
+            if (r) { k.v[0] += 0x9E3779B9u; k.v[1] += 0xBB67AE85u; }
+            const uint64_t p0 = (uint64_t)0xD2511F53u * c.v[0], p1 = (uint64_t)0xCD9E8D57u * c.v[2];
+            const ctr_type n = {{(uint32_t)(p1 >> 32) ^ c.v[1] ^ k.v[0], (uint32_t)p1,
+                                 (uint32_t)(p0 >> 32) ^ c.v[3] ^ k.v[1], (uint32_t)p0}};
+            c = n;
+        }
+        return c;
+    }
+};
+}  // namespace r123
+
+namespace RandBLAS {
+
+namespace exceptions {
+class Error : public std::exception {
+public:
+    explicit Error(std::string msg) : msg_(std::move(msg)) {}
+    const char *what() const noexcept override { return msg_.c_str(); }
+private:
+    std::string msg_;
+};
+}  // namespace exceptions
+
+namespace detail {
+inline void check(int rc) {
+    if (rc != RBH_OK) throw exceptions::Error(rbh_last_error());
+}
+inline void require(bool cond, const char *text, const char *func) {
+    if (!cond)
+        throw exceptions::Error(std::string("(") + text + ") was required, but did not hold, in function " + func);
+}
+}  // namespace detail
+#define RBH_CXX_REQUIRE(c) ::RandBLAS::detail::require((c), #c, __func__)
+
+enum class MajorAxis : char { Short = 'S', Long = 'L', Undefined = 'U' };
+
+template <typename RNG = r123::Philox4x32>
+struct RNGState {
+    using generator = RNG;
+    using ctr_type = typename RNG::ctr_type;
+    using key_type = typename RNG::key_type;
+    using ctr_uint = typename ctr_type::value_type;
+    using key_uint = typename key_type::value_type;
+    static const int len_c = ctr_type::static_size;
+    static const int len_k = key_type::static_size;
+    ctr_type counter;
+    key_type key;
+    RNGState() : counter{{0}}, key{{0}} {}
+    RNGState(key_type const &k) : counter{{0}}, key(k) {}
+    RNGState(ctr_type const &c, key_type const &k) : counter(c), key(k) {}
+    RNGState(key_uint k) : counter{{0}}, key{{k}} {}
+};
+
+namespace detail {
+template <typename RNG>
+inline rbh_state c_state(const RNGState<RNG> &s) {
+    rbh_state o;
+    std::memcpy(o.counter, s.counter.v, sizeof o.counter);
+    std::memcpy(o.key, s.key.v, sizeof o.key);
+    return o;
+}
+template <typename RNG>
+inline RNGState<RNG> from_c(const rbh_state &s) {
+    RNGState<RNG> o;
+    std::memcpy(o.counter.v, s.counter, sizeof s.counter);
+    std::memcpy(o.key.v, s.key, sizeof s.key);
+    return o;
+}
+}  // namespace detail
+
+// ---------------------------------------------------------------------------------------------
+// Dense operators
+// ---------------------------------------------------------------------------------------------
+enum class DenseDistName : char { Gaussian = 'G', Uniform = 'U', BlackBox = 'B' };
+
+struct DenseDist {
+    const int64_t n_rows;
+    const int64_t n_cols;
+    const DenseDistName family;
+    const MajorAxis major_axis;
+    DenseDist(int64_t n_rows, int64_t n_cols, DenseDistName dn = DenseDistName::Gaussian)
+        : n_rows(n_rows), n_cols(n_cols), family(dn),
+          major_axis(dn == DenseDistName::BlackBox ? MajorAxis::Undefined : MajorAxis::Long) {}
+    DenseDist(int64_t n_rows, int64_t n_cols, DenseDistName dn, MajorAxis ma)
+        : n_rows(n_rows), n_cols(n_cols), family(dn), major_axis(ma) {
+        if (dn == DenseDistName::BlackBox) RBH_CXX_REQUIRE(ma == MajorAxis::Undefined);
+        else RBH_CXX_REQUIRE(ma != MajorAxis::Undefined);
+    }
+};
+
+inline rbh_dense_dist c_dist(const DenseDist &D) {
+    return rbh_dense_dist{D.n_rows, D.n_cols, (char)D.family, (char)D.major_axis};
+}
+
+inline blas::Layout dist_to_layout(const DenseDist &D) {
+    RBH_CXX_REQUIRE(D.major_axis != MajorAxis::Undefined);
+    const bool is_wide = D.n_rows < D.n_cols, fa_long = D.major_axis == MajorAxis::Long;
+    if (is_wide && fa_long) return blas::Layout::RowMajor;
+    if (is_wide) return blas::Layout::ColMajor;
+    if (fa_long) return blas::Layout::ColMajor;
+    return blas::Layout::RowMajor;
+}
+
+inline int64_t major_axis_length(const DenseDist &D) {
+    RBH_CXX_REQUIRE(D.major_axis != MajorAxis::Undefined);
+    return D.major_axis == MajorAxis::Long ? std::max(D.n_rows, D.n_cols) : std::min(D.n_rows, D.n_cols);
+}
+
+template <typename T>
+inline T isometry_scale_factor(DenseDist D) {
+    if (D.family == DenseDistName::BlackBox) throw std::runtime_error("Unrecognized distribution.");
+    return std::pow((T)std::min(D.n_rows, D.n_cols), -0.5);
+}
+
+namespace dense {
+template <typename RNG>
+inline RNGState<RNG> compute_next_state(const DenseDist &dist, const RNGState<RNG> &state) {
+    const rbh_dense_dist d = c_dist(dist);
+    const rbh_state s = detail::c_state(state);
+    rbh_state n;
+    detail::check(rbh_dense_next_state(&d, &s, &n));
+    return detail::from_c<RNG>(n);
+}
+}  // namespace dense
+
+template <typename T, typename RNG = r123::Philox4x32>
+struct DenseSkOp {
+    using state_t = RNGState<RNG>;
+    using scalar_t = T;
+    const int64_t n_rows;
+    const int64_t n_cols;
+    const DenseDist dist;
+    const RNGState<RNG> seed_state;
+    const RNGState<RNG> next_state;
+    T *buff = nullptr;
+    blas::Layout layout;
+    bool del_buff_on_destruct = false;
+
+    DenseSkOp(int64_t n_rows, int64_t n_cols, DenseDist dist, RNGState<RNG> const &seed_state,
+              RNGState<RNG> const &next_state, T *buff, blas::Layout layout, bool del_buff_on_destruct)
+        : n_rows(n_rows), n_cols(n_cols), dist(dist), seed_state(seed_state), next_state(next_state), buff(buff),
+          layout(layout), del_buff_on_destruct(del_buff_on_destruct) {}
+
+    DenseSkOp(DenseDist dist, RNGState<RNG> const &state)
+        : n_rows(dist.n_rows), n_cols(dist.n_cols), dist(dist), seed_state(state),
+          next_state(dense::compute_next_state(dist, state)), buff(nullptr),
+          layout(dist.major_axis == MajorAxis::Undefined ? blas::Layout::ColMajor : dist_to_layout(dist)) {
+        RBH_CXX_REQUIRE(this->dist.n_rows > 0);
+        RBH_CXX_REQUIRE(this->dist.n_cols > 0);
+        if (dist.family == DenseDistName::BlackBox) RBH_CXX_REQUIRE(this->buff != nullptr);
+    }
+    ~DenseSkOp() {
+        if (del_buff_on_destruct) delete[] buff;
+    }
+};
+
+namespace detail {
+template <typename T> struct Api;
+template <> struct Api<double> {
+    static int fill_dense(char l, const rbh_dense_dist *D, int64_t r, int64_t c, int64_t ro, int64_t co, double *b,
+                          const rbh_state *s, rbh_state *n) { return rbh_fill_dense_f64(l, D, r, c, ro, co, b, s, n, nullptr); }
+    static int fill_sparse(const rbh_sparse_dist *D, const rbh_state *s, int64_t *r, int64_t *c, double *v) {
+        return rbh_fill_sparse_f64(D, s, r, c, v, nullptr);
+    }
+    static constexpr auto lskge3 = rbh_lskge3_f64;
+    static constexpr auto rskge3 = rbh_rskge3_f64;
+    static constexpr auto lskges = rbh_lskges_f64;
+    static constexpr auto rskges = rbh_rskges_f64;
+    static constexpr auto sym = rbh_require_symmetric_f64;
+};
+template <> struct Api<float> {
+    static int fill_dense(char l, const rbh_dense_dist *D, int64_t r, int64_t c, int64_t ro, int64_t co, float *b,
+                          const rbh_state *s, rbh_state *n) { return rbh_fill_dense_f32(l, D, r, c, ro, co, b, s, n, nullptr); }
+    static int fill_sparse(const rbh_sparse_dist *D, const rbh_state *s, int64_t *r, int64_t *c, float *v) {
+        return rbh_fill_sparse_f32(D, s, r, c, v, nullptr);
+    }
+    static constexpr auto lskge3 = rbh_lskge3_f32;
+    static constexpr auto rskge3 = rbh_rskge3_f32;
+    static constexpr auto lskges = rbh_lskges_f32;
+    static constexpr auto rskges = rbh_rskges_f32;
+    static constexpr auto sym = rbh_require_symmetric_f32;
+};
+}  // namespace detail
+
+template <typename T, typename RNG = r123::Philox4x32>
+RNGState<RNG> fill_dense(blas::Layout layout, const DenseDist &D, int64_t n_rows, int64_t n_cols, int64_t ro_s,
+                         int64_t co_s, T *buff, const RNGState<RNG> &seed) {
+    const rbh_dense_dist d = c_dist(D);
+    const rbh_state s = detail::c_state(seed);
+    rbh_state n;
+    detail::check(detail::Api<T>::fill_dense((char)layout, &d, n_rows, n_cols, ro_s, co_s, buff, &s, &n));
+    return detail::from_c<RNG>(n);
+}
+
+template <typename T, typename RNG = r123::Philox4x32>
+RNGState<RNG> fill_dense(const DenseDist &D, T *buff, const RNGState<RNG> &seed) {
+    return fill_dense(dist_to_layout(D), D, D.n_rows, D.n_cols, 0, 0, buff, seed);
+}
+
+template <typename DenseSkOpT>
+void fill_dense(DenseSkOpT &S) {
+    using T = typename DenseSkOpT::scalar_t;
+    RBH_CXX_REQUIRE(S.buff == nullptr);
+    RBH_CXX_REQUIRE(S.dist.family != DenseDistName::BlackBox);
+    S.buff = new T[S.dist.n_rows * S.dist.n_cols];
+    fill_dense(S.dist, S.buff, S.seed_state);
+    S.del_buff_on_destruct = true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Sparse operators
+// ---------------------------------------------------------------------------------------------
+struct SparseDist {
+    const int64_t n_rows;
+    const int64_t n_cols;
+    const int64_t vec_nnz;
+    const MajorAxis major_axis = MajorAxis::Short;
+};
+
+inline rbh_sparse_dist c_dist(const SparseDist &D) {
+    return rbh_sparse_dist{D.n_rows, D.n_cols, D.vec_nnz, (char)D.major_axis};
+}
+
+template <typename T>
+inline T isometry_scale_factor(SparseDist D) {
+    const T vec_nnz = (T)D.vec_nnz;
+    if (D.major_axis == MajorAxis::Short) return std::pow(vec_nnz, -0.5);
+    const T minor_ax_len = (T)std::min(D.n_rows, D.n_cols), major_ax_len = (T)std::max(D.n_rows, D.n_cols);
+    return std::sqrt(major_ax_len / (vec_nnz * minor_ax_len));
+}
+
+namespace sparse {
+template <typename RNG>
+inline RNGState<RNG> compute_next_state(const SparseDist &dist, const RNGState<RNG> &state) {
+    const rbh_sparse_dist d = c_dist(dist);
+    const rbh_state s = detail::c_state(state);
+    rbh_state n;
+    detail::check(rbh_sparse_next_state(&d, &s, &n));
+    return detail::from_c<RNG>(n);
+}
+}  // namespace sparse
+
+template <typename T, typename RNG = r123::Philox4x32, typename sint_t = int64_t>
+struct SparseSkOp {
+    static_assert(std::is_same<sint_t, int64_t>::value, "librandblas_hip stores SparseSkOp indices as int64_t");
+    using index_t = sint_t;
+    using state_t = RNGState<RNG>;
+    using scalar_t = T;
+    const int64_t n_rows;
+    const int64_t n_cols;
+    const SparseDist dist;
+    const RNGState<RNG> seed_state;
+    const RNGState<RNG> next_state;
+    const bool own_memory = true;
+    bool known_filled = false;
+    sint_t *rows = nullptr;
+    sint_t *cols = nullptr;
+    T *vals = nullptr;
+
+    SparseSkOp(SparseDist dist, const RNGState<RNG> &state, sint_t *rows, sint_t *cols, T *vals,
+               bool known_filled = true)
+        : n_rows(dist.n_rows), n_cols(dist.n_cols), dist(dist), seed_state(state),
+          next_state(sparse::compute_next_state(dist, state)), own_memory(false), known_filled(known_filled),
+          rows(rows), cols(cols), vals(vals) {
+        RBH_CXX_REQUIRE(this->dist.n_rows > 0);
+        RBH_CXX_REQUIRE(this->dist.n_cols > 0);
+        RBH_CXX_REQUIRE(this->dist.vec_nnz > 0);
+    }
+    SparseSkOp(SparseDist dist, uint32_t key, sint_t *rows, sint_t *cols, T *vals)
+        : SparseSkOp(dist, RNGState<RNG>(key), rows, cols, vals) {}
+    SparseSkOp(SparseDist dist, const RNGState<RNG> &state)
+        : n_rows(dist.n_rows), n_cols(dist.n_cols), dist(dist), seed_state(state),
+          next_state(sparse::compute_next_state(dist, state)), own_memory(true) {
+        RBH_CXX_REQUIRE(this->dist.n_rows > 0);
+        RBH_CXX_REQUIRE(this->dist.n_cols > 0);
+        RBH_CXX_REQUIRE(this->dist.vec_nnz > 0);
+        const int64_t nnz = nnz_count();
+        rows = new sint_t[nnz];
+        cols = new sint_t[nnz];
+        vals = new T[nnz];
+    }
+    SparseSkOp(SparseDist dist, uint32_t key) : SparseSkOp(dist, RNGState<RNG>(key)) {}
+    ~SparseSkOp() {
+        if (own_memory) {
+            delete[] rows;
+            delete[] cols;
+            delete[] vals;
+        }
+    }
+    int64_t nnz_count() const {
+        const rbh_sparse_dist d = c_dist(dist);
+        return rbh_sparse_nnz(&d);
+    }
+};
+
+template <typename SparseSkOpT>
+void fill_sparse(SparseSkOpT &S) {
+    using T = typename SparseSkOpT::scalar_t;
+    const rbh_sparse_dist d = c_dist(S.dist);
+    const rbh_state s = detail::c_state(S.seed_state);
+    detail::check(detail::Api<T>::fill_sparse(&d, &s, S.rows, S.cols, S.vals));
+    S.known_filled = true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// sketch_general (skge.hh:771-1214)
+// ---------------------------------------------------------------------------------------------
+namespace detail {
+template <typename T, typename RNG>
+void lsk(blas::Layout layout, blas::Op opS, blas::Op opA, int64_t d, int64_t n, int64_t m, T alpha,
+         DenseSkOp<T, RNG> &S, int64_t ro_s, int64_t co_s, const T *A, int64_t lda, T beta, T *B, int64_t ldb) {
+    const rbh_dense_dist dd = c_dist(S.dist);
+    const rbh_state s = c_state(S.seed_state);
+    check(Api<T>::lskge3((char)layout, (char)opS, (char)opA, d, n, m, alpha, &dd, &s, S.buff, (char)S.layout, ro_s,
+                         co_s, A, lda, beta, B, ldb, nullptr));
+}
+template <typename T, typename RNG, typename sint_t>
+void lsk(blas::Layout layout, blas::Op opS, blas::Op opA, int64_t d, int64_t n, int64_t m, T alpha,
+         SparseSkOp<T, RNG, sint_t> &S, int64_t ro_s, int64_t co_s, const T *A, int64_t lda, T beta, T *B,
+         int64_t ldb) {
+    const rbh_sparse_dist dd = c_dist(S.dist);
+    const rbh_state s = c_state(S.seed_state);
+    const bool have = S.known_filled;
+    check(Api<T>::lskges((char)layout, (char)opS, (char)opA, d, n, m, alpha, &dd, &s, have ? S.nnz_count() : 0,
+                         have ? S.rows : nullptr, have ? S.cols : nullptr, have ? S.vals : nullptr, ro_s, co_s, A,
+                         lda, beta, B, ldb, nullptr));
+}
+template <typename T, typename RNG>
+void rsk(blas::Layout layout, blas::Op opA, blas::Op opS, int64_t m, int64_t d, int64_t n, T alpha, const T *A,
+         int64_t lda, DenseSkOp<T, RNG> &S, int64_t ro_s, int64_t co_s, T beta, T *B, int64_t ldb) {
+    const rbh_dense_dist dd = c_dist(S.dist);
+    const rbh_state s = c_state(S.seed_state);
+    check(Api<T>::rskge3((char)layout, (char)opA, (char)opS, m, d, n, alpha, A, lda, &dd, &s, S.buff,
+                         (char)S.layout, ro_s, co_s, beta, B, ldb, nullptr));
+}
+template <typename T, typename RNG, typename sint_t>
+void rsk(blas::Layout layout, blas::Op opA, blas::Op opS, int64_t m, int64_t d, int64_t n, T alpha, const T *A,
+         int64_t lda, SparseSkOp<T, RNG, sint_t> &S, int64_t ro_s, int64_t co_s, T beta, T *B, int64_t ldb) {
+    const rbh_sparse_dist dd = c_dist(S.dist);
+    const rbh_state s = c_state(S.seed_state);
+    const bool have = S.known_filled;
+    check(Api<T>::rskges((char)layout, (char)opA, (char)opS, m, d, n, alpha, A, lda, &dd, &s,
+                         have ? S.nnz_count() : 0, have ? S.rows : nullptr, have ? S.cols : nullptr,
+                         have ? S.vals : nullptr, ro_s, co_s, beta, B, ldb, nullptr));
+}
+}  // namespace detail
+
+// Left, submatrix: B = alpha op(submat(S)) op(A) + beta B
+template <typename T, typename SKOP>
+inline void sketch_general(blas::Layout layout, blas::Op opS, blas::Op opA, int64_t d, int64_t n, int64_t m, T alpha,
+                           SKOP &S, int64_t ro_s, int64_t co_s, const T *A, int64_t lda, T beta, T *B, int64_t ldb) {
+    detail::lsk(layout, opS, opA, d, n, m, alpha, S, ro_s, co_s, A, lda, beta, B, ldb);
+}
+
+// Right, submatrix: B = alpha op(A) op(submat(S)) + beta B
+template <typename T, typename SKOP>
+inline void sketch_general(blas::Layout layout, blas::Op opA, blas::Op opS, int64_t m, int64_t d, int64_t n, T alpha,
+                           const T *A, int64_t lda, SKOP &S, int64_t ro_s, int64_t co_s, T beta, T *B, int64_t ldb) {
+    detail::rsk(layout, opA, opS, m, d, n, alpha, A, lda, S, ro_s, co_s, beta, B, ldb);
+}
+
+// Left, full operator (skge.hh:1088-1112)
+template <typename T, typename SKOP>
+inline void sketch_general(blas::Layout layout, blas::Op opS, blas::Op opA, int64_t d, int64_t n, int64_t m, T alpha,
+                           SKOP &S, const T *A, int64_t lda, T beta, T *B, int64_t ldb) {
+    if (opS == blas::Op::NoTrans) {
+        RBH_CXX_REQUIRE(S.dist.n_rows == d);
+        RBH_CXX_REQUIRE(S.dist.n_cols == m);
+    } else {
+        RBH_CXX_REQUIRE(S.dist.n_rows == m);
+        RBH_CXX_REQUIRE(S.dist.n_cols == d);
+    }
+    sketch_general(layout, opS, opA, d, n, m, alpha, S, (int64_t)0, (int64_t)0, A, lda, beta, B, ldb);
+}
+
+// Right, full operator (skge.hh:1190-1214)
+template <typename T, typename SKOP>
+inline void sketch_general(blas::Layout layout, blas::Op opA, blas::Op opS, int64_t m, int64_t d, int64_t n, T alpha,
+                           const T *A, int64_t lda, SKOP &S, T beta, T *B, int64_t ldb) {
+    if (opS == blas::Op::NoTrans) {
+        RBH_CXX_REQUIRE(S.dist.n_rows == n);
+        RBH_CXX_REQUIRE(S.dist.n_cols == d);
+    } else {
+        RBH_CXX_REQUIRE(S.dist.n_rows == d);
+        RBH_CXX_REQUIRE(S.dist.n_cols == n);
+    }
+    sketch_general(layout, opA, opS, m, d, n, alpha, A, lda, S, (int64_t)0, (int64_t)0, beta, B, ldb);
+}
+
+// ---------------------------------------------------------------------------------------------
+// sketch_symmetric (sksy.hh:165-537): require_symmetric (on the device) + sketch_general
+// ---------------------------------------------------------------------------------------------
+namespace util {
+template <typename T>
+void require_symmetric(blas::Layout layout, const T *A, int64_t n, int64_t lda, T tol) {
+    detail::check(detail::Api<T>::sym((char)layout, A, n, lda, tol, nullptr));
+}
+}  // namespace util
+
+// B = alpha A op(submat(S)) + beta B   (A symmetric n x n in general storage)
+template <typename T, typename SKOP>
+inline void sketch_symmetric(blas::Layout layout, int64_t n, int64_t d, T alpha, const T *A, int64_t lda, SKOP &S,
+                             int64_t ro_s, int64_t co_s, T beta, T *B, int64_t ldb, T sym_check_tol = 0) {
+    util::require_symmetric(layout, A, n, lda, sym_check_tol);
+    sketch_general(layout, blas::Op::NoTrans, blas::Op::NoTrans, n, d, n, alpha, A, lda, S, ro_s, co_s, beta, B, ldb);
+}
+
+// B = alpha submat(S) A + beta B
+template <typename T, typename SKOP>
+inline void sketch_symmetric(blas::Layout layout, int64_t d, int64_t n, T alpha, SKOP &S, int64_t ro_s, int64_t co_s,
+                             const T *A, int64_t lda, T beta, T *B, int64_t ldb, T sym_check_tol = 0) {
+    util::require_symmetric(layout, A, n, lda, sym_check_tol);
+    sketch_general(layout, blas::Op::NoTrans, blas::Op::NoTrans, d, n, n, alpha, S, ro_s, co_s, A, lda, beta, B, ldb);
+}
+
+// B = alpha A S + beta B
+template <typename T, typename SKOP>
+inline void sketch_symmetric(blas::Layout layout, T alpha, const T *A, int64_t lda, SKOP &S, T beta, T *B,
+                             int64_t ldb, T sym_check_tol = 0) {
+    const int64_t n = S.dist.n_rows, d = S.dist.n_cols;
+    util::require_symmetric(layout, A, n, lda, sym_check_tol);
+    sketch_general(layout, blas::Op::NoTrans, blas::Op::NoTrans, n, d, n, alpha, A, lda, S, (int64_t)0, (int64_t)0,
+                   beta, B, ldb);
+}
+
+// B = alpha S A + beta B
+template <typename T, typename SKOP>
+inline void sketch_symmetric(blas::Layout layout, T alpha, SKOP &S, const T *A, int64_t lda, T beta, T *B,
+                             int64_t ldb, T sym_check_tol = 0) {
+    const int64_t d = S.dist.n_rows, n = S.dist.n_cols;
+    util::require_symmetric(layout, A, n, lda, sym_check_tol);
+    sketch_general(layout, blas::Op::NoTrans, blas::Op::NoTrans, d, n, n, alpha, S, (int64_t)0, (int64_t)0, A, lda,
+                   beta, B, ldb);
+}
+
+}  // namespace RandBLAS
