@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -550,6 +551,7 @@ int sparse_common(SparseApply &p, const rbh_sparse_dist *D, const rbh_state *see
         dr = t0; dc = t1; dv = t2;
     }
     if (p.alpha == 0.0) nnz = 0;   // left_spmm returns after the beta scaling (:134-135)
+    if (const char *ab = getenv("RBH_SASO_ABLATE")) p.ablate = atoi(ab);   // diagnostics only
     hipError_t e = run_sparse_apply_t<T>(p, (const int64_t *)dr, (const int64_t *)dc, (const T *)dv, nnz, s);
     if (gen_ws) (void)hipFreeAsync(gen_ws, s);
     RBH_HIP(e);

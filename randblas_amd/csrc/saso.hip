@@ -102,143 +102,277 @@ hipError_t launch_fill_sparse_f32(const SparseGen &g, int64_t *rows, int64_t *co
 }
 
 // ------------------------------------------------------------------------------------------
-// 2. CSR of op(submat(S)) with alpha folded in
+// 2. Chunked CSR of op(submat(S)), alpha folded in.
+//    The contracted index k is cut into chunks of SP_KC; "virtual row" v = (k / SP_KC) * M + i.
+//    Sorting by key = v * SP_KC + (k % SP_KC) orders entries by (chunk, output row, k), so the
+//    entries of output row i inside chunk c are contiguous and ascending in k, and walking the
+//    chunks in order walks every row in ascending k: the reference's accumulation order.
 // ------------------------------------------------------------------------------------------
+constexpr int SP_KC = 128;        // contracted indices per chunk (LDS panel depth)
+
 template <typename T>
 __global__ void coo_keys_kernel(int64_t nnz, const int64_t *rows, const int64_t *cols, const T *vals, int64_t ro,
-                                int64_t co, int64_t win_r, int64_t win_c, int transposed, int64_t K, T alpha,
+                                int64_t co, int64_t win_r, int64_t win_c, int transposed, int64_t M, T alpha,
                                 uint64_t *keys, T *kv) {
     const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (e >= nnz) return;
     const int64_t wr = rows[e] - ro, wc = cols[e] - co;
     const bool in = wr >= 0 && wr < win_r && wc >= 0 && wc < win_c;
-    const int64_t i = transposed ? wc : wr;
-    const int64_t k = transposed ? wr : wc;
-    keys[e] = in ? (uint64_t)i * (uint64_t)K + (uint64_t)k : ~(uint64_t)0;
+    const uint64_t i = (uint64_t)(transposed ? wc : wr);
+    const uint64_t k = (uint64_t)(transposed ? wr : wc);
+    const uint64_t v = (k / SP_KC) * (uint64_t)M + i;
+    keys[e] = in ? v * SP_KC + (k % SP_KC) : ~(uint64_t)0;
     kv[e] = alpha * vals[e];
 }
 
-// rowptr[i] = first sorted position whose key >= i*K (invalid keys sort last).
-__global__ void rowptr_kernel(int64_t nnz, const uint64_t *keys, int64_t M, int64_t K, int64_t *rowptr,
-                              int32_t *kidx) {
+// vrp[v] = first sorted position whose virtual row is >= v (invalid keys sort last); kl = k % SP_KC.
+__global__ void rowptr_kernel(int64_t nnz, const uint64_t *keys, int64_t NV, int32_t *vrp, uint16_t *kl) {
     const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (e > nnz) return;
     const uint64_t inval = ~(uint64_t)0;
-    const int64_t cur = (e < nnz && keys[e] != inval) ? (int64_t)(keys[e] / (uint64_t)K) : M;
-    const int64_t prev = (e == 0) ? -1 : ((keys[e - 1] != inval) ? (int64_t)(keys[e - 1] / (uint64_t)K) : M);
-    for (int64_t i = prev + 1; i <= cur && i <= M; ++i) rowptr[i] = e;
-    if (e < nnz && keys[e] != inval) kidx[e] = (int32_t)(keys[e] % (uint64_t)K);
+    const int64_t cur = (e < nnz && keys[e] != inval) ? (int64_t)(keys[e] / SP_KC) : NV;
+    const int64_t prev = (e == 0) ? -1 : ((keys[e - 1] != inval) ? (int64_t)(keys[e - 1] / SP_KC) : NV);
+    for (int64_t v = prev + 1; v <= cur && v <= NV; ++v) vrp[v] = (int32_t)e;
+    if (e < nnz && keys[e] != inval) kl[e] = (uint16_t)(keys[e] % SP_KC);
 }
 
 // ------------------------------------------------------------------------------------------
-// 3. Apply: C(i,j) = beta*C(i,j) + sum_{e in row i, ascending k} kv[e] * Y(k_e, j)
+// 3. Apply: C(i,j) = beta*C(i,j) + sum_{k ascending} kv * Y(k, j)
+//
+// Workgroup = 16 waves; it owns 512 output rows x 64 output columns. Lane l works on output column
+// j0 + l and a wave owns 32 consecutive output rows, so every entry a wave processes is the same
+// for all its lanes: the row walk is uniform (scalar loop bounds, no divergence), the entry is a
+// broadcast LDS read, and the only per-lane work is one LDS read of Y, one multiply and one add.
+// Per chunk of SP_KC contracted indices the workgroup holds in LDS:
+//   * the Y panel, column-major [64 columns][SP_KC + 1] (odd stride: 64 lanes reading one k of 64
+//     columns are conflict-free);
+//   * the chunk's CSR entries of its 512 rows (k % SP_KC as u16, value) and their row pointers.
+// The next chunk's panel, entries and row pointers are loaded into registers while the current
+// chunk is consumed. Each lane keeps its 32 running sums in registers across all chunks.
 // ------------------------------------------------------------------------------------------
-constexpr int SP_J = 16;     // output columns per workgroup
-constexpr int SP_KC = 256;   // contracted indices staged per chunk
-constexpr int SP_NT = 512;   // threads per workgroup
+constexpr int SA_NT = 1024;                  // threads per workgroup
+constexpr int SA_J = 64;                     // output columns per workgroup (one per lane)
+constexpr int SA_R = 32;                     // output rows per wave
+constexpr int SA_ROWS = SA_NT / 64 * SA_R;   // 512 output rows per workgroup
+constexpr int SA_LDP = SP_KC + 1;            // panel column stride (elements)
+constexpr int SA_EMAX = 2048;                // entries staged in LDS per chunk (more: extra windows)
+constexpr int SA_ESLOT = SA_EMAX / SA_NT;    // entry prefetch slots per thread
 
-template <typename T> struct SpLds { static constexpr int LD = SP_J + 16 / (int)sizeof(T); };  // padded k-row
+template <typename T> struct PanelVec;
+template <> struct PanelVec<double> { typedef double v __attribute__((ext_vector_type(2))); static constexpr int N = 2; };
+template <> struct PanelVec<float> { typedef float v __attribute__((ext_vector_type(4))); static constexpr int N = 4; };
 
-template <typename T, int R>
-__global__ __launch_bounds__(SP_NT) void saso_apply_kernel(const SparseApply p, const int64_t *rowptr,
-                                                            const int32_t *kidx, const T *kv) {
-    constexpr int LD = SpLds<T>::LD;
-    __shared__ __attribute__((aligned(16))) T ys[2][SP_KC * LD];
-    const int tid = threadIdx.x;
-    const int64_t j0 = (int64_t)blockIdx.x * SP_J;
-    const int64_t rb0 = (int64_t)blockIdx.y * (SP_NT * R);
+template <typename T, bool VP>
+struct SaPrefetch {
+    static constexpr int VEC = PanelVec<T>::N;
+    static constexpr int NPV = SA_J * SP_KC / VEC / SA_NT;   // 16-B panel loads per thread
+    static constexpr int NPS = SA_J * SP_KC / SA_NT;         // scalar panel loads per thread
+    typename PanelVec<T>::v pv[VP ? NPV : 1];
+    T ps[VP ? 1 : NPS];
+    uint16_t ek[SA_ESLOT];
+    T ev[SA_ESLOT];
+    int32_t rp0;
+    int32_t ebase, ecount;
+};
+
+template <typename T, bool VP>
+__device__ __forceinline__ void sa_load(SaPrefetch<T, VP> &f, const SparseApply &p, const int32_t *vrp,
+                                        const uint16_t *kl, const T *kv, int64_t c, int64_t j0, int64_t rb0,
+                                        int nrows, int tid) {
     const T *Y = (const T *)p.Y;
-    T *C = (T *)p.C;
-    const T beta = (T)p.beta;
-
-    int64_t cur[R], end[R];
-    T acc[R][SP_J];
+    const int64_t kc0 = c * SP_KC;
+    if (VP) {
+        constexpr int VEC = PanelVec<T>::N;
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int64_t i = rb0 + tid + r * SP_NT;
-        cur[r] = (i < p.M) ? rowptr[i] : 0;
-        end[r] = (i < p.M) ? rowptr[i + 1] : 0;
+        for (int q = 0; q < SaPrefetch<T, VP>::NPV; ++q) {
+            const int idx = tid + q * SA_NT;
+            const int cc = idx / (SP_KC / VEC);
+            const int kk = (idx % (SP_KC / VEC)) * VEC;
+            const int64_t gk = kc0 + kk, gj = j0 + cc;
+            typename PanelVec<T>::v x;
+            if (gk < p.K && gj < p.N) x = *reinterpret_cast<const typename PanelVec<T>::v *>(Y + gk + gj * p.ysj);
+            else for (int t = 0; t < VEC; ++t) x[t] = (T)0;
+            f.pv[q] = x;
+        }
+    } else {
+        const bool kfast = p.ysk == 1;
 #pragma unroll
-        for (int c = 0; c < SP_J; ++c) {
-            const int64_t j = j0 + c;
-            T v = (T)0;
-            if (i < p.M && j < p.N && beta != (T)0) v = beta * C[i * p.crs + j * p.ccs];
-            acc[r][c] = v;
+        for (int q = 0; q < SaPrefetch<T, VP>::NPS; ++q) {
+            const int idx = tid + q * SA_NT;
+            const int cc = kfast ? idx / SP_KC : idx % SA_J;
+            const int kk = kfast ? idx % SP_KC : idx / SA_J;
+            const int64_t gk = kc0 + kk, gj = j0 + cc;
+            f.ps[q] = (gk < p.K && gj < p.N) ? Y[gk * p.ysk + gj * p.ysj] : (T)0;
         }
     }
-
-    const int64_t nkc = (p.K + SP_KC - 1) / SP_KC;
-    // stage chunk 0
-    auto stage = [&](int buf, int64_t kc0) {
-        // element (k, c): Y[(kc0+k)*ysk + (j0+c)*ysj]; walk k fastest when ysk == 1
-        const bool kfast = p.ysk == 1;
-        for (int e = tid; e < SP_KC * SP_J; e += SP_NT) {
-            const int k = kfast ? e % SP_KC : e / SP_J;
-            const int c = kfast ? e / SP_KC : e % SP_J;
-            const int64_t gk = kc0 + k, gj = j0 + c;
-            ys[buf][k * LD + c] = (gk < p.K && gj < p.N) ? Y[gk * p.ysk + gj * p.ysj] : (T)0;
+    const int64_t v0 = c * p.M + rb0;
+    const int32_t base = vrp[v0];
+    f.ebase = base;
+    f.ecount = vrp[v0 + nrows] - base;
+    f.rp0 = vrp[v0 + (tid < nrows ? tid : nrows)] - base;   // row pointers 0..nrows (rest: end)
+#pragma unroll
+    for (int q = 0; q < SA_ESLOT; ++q) {
+        const int e = tid + q * SA_NT;
+        if (e < f.ecount && e < SA_EMAX) {
+            f.ek[q] = kl[base + e];
+            f.ev[q] = kv[base + e];
         }
-    };
-    stage(0, 0);
-    __syncthreads();
-    for (int64_t kc = 0; kc < nkc; ++kc) {
-        const int buf = (int)(kc & 1);
-        const int64_t kc0 = kc * SP_KC, kc1 = kc0 + SP_KC;
-        if (kc + 1 < nkc) stage(buf ^ 1, kc1);
+    }
+}
+
+template <typename T, bool VP>
+__device__ __forceinline__ void sa_store(const SaPrefetch<T, VP> &f, T *panel, uint16_t *ek, T *ev, int32_t *rp,
+                                         const SparseApply &p, int tid) {
+    if (VP) {
+        constexpr int VEC = PanelVec<T>::N;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            while (cur[r] < end[r]) {
-                const int32_t k = kidx[cur[r]];
-                if (k >= kc1) break;
-                const T v = kv[cur[r]];
-                const T *yrow = &ys[buf][(k - kc0) * LD];
+        for (int q = 0; q < SaPrefetch<T, VP>::NPV; ++q) {
+            const int idx = tid + q * SA_NT;
+            const int cc = idx / (SP_KC / VEC);
+            const int kk = (idx % (SP_KC / VEC)) * VEC;
 #pragma unroll
-                for (int c = 0; c < SP_J; ++c) {
+            for (int t = 0; t < VEC; ++t) panel[cc * SA_LDP + kk + t] = f.pv[q][t];
+        }
+    } else {
+        const bool kfast = p.ysk == 1;
+#pragma unroll
+        for (int q = 0; q < SaPrefetch<T, VP>::NPS; ++q) {
+            const int idx = tid + q * SA_NT;
+            const int cc = kfast ? idx / SP_KC : idx % SA_J;
+            const int kk = kfast ? idx % SP_KC : idx / SA_J;
+            panel[cc * SA_LDP + kk] = f.ps[q];
+        }
+    }
+    if (tid <= SA_ROWS) rp[tid] = f.rp0;
+#pragma unroll
+    for (int q = 0; q < SA_ESLOT; ++q) {
+        const int e = tid + q * SA_NT;
+        if (e < f.ecount && e < SA_EMAX) {
+            ek[e] = f.ek[q];
+            ev[e] = f.ev[q];
+        }
+    }
+}
+
+// One chunk (or one window [wlo, whi) of its entries, held in LDS at e - wlo): the wave walks its
+// 32 rows; all bounds are wave-uniform (read once per lane, then readlane'd into scalars).
+template <typename T>
+__device__ __forceinline__ void sa_compute(T (&acc)[SA_R], const T *panel, const uint16_t *ek, const T *ev,
+                                           const int32_t *rp, int wlo, int whi, int wrow, int lane) {
+    const T *pcol = panel + lane * SA_LDP;
+    const int myrp = rp[wrow + (lane < SA_R ? lane : SA_R)];   // this wave's 33 row pointers
+#pragma unroll
+    for (int r = 0; r < SA_R; ++r) {
+        const int e0 = max(__builtin_amdgcn_readlane(myrp, r), wlo) - wlo;
+        const int e1 = min(__builtin_amdgcn_readlane(myrp, r + 1), whi) - wlo;
+        T s = acc[r];
+        for (int e = e0; e < e1; ++e) {
 #if defined(__clang__)
 #pragma clang fp contract(off)
 #endif
-                    const T prod = v * yrow[c];
-                    acc[r][c] = acc[r][c] + prod;
-                }
-                cur[r]++;
-            }
+            const T prod = ev[e] * pcol[ek[e]];
+            s = s + prod;
         }
+        acc[r] = s;
+    }
+}
+
+template <typename T, bool VP>
+__global__ __launch_bounds__(SA_NT) void saso_apply_kernel(const SparseApply p, const int32_t *vrp, const uint16_t *kl,
+                                                            const T *kv, int64_t nchunks, int64_t nrb) {
+    // one LDS array, carved (panel | values | row pointers | u16 k)
+    constexpr int PANEL = SA_J * SA_LDP;
+    constexpr size_t BYTES = PANEL * sizeof(T) + SA_EMAX * sizeof(T) + (SA_ROWS + 1) * sizeof(int32_t) +
+                             SA_EMAX * sizeof(uint16_t);
+    __shared__ __attribute__((aligned(16))) char smem[BYTES];
+    T *panel = reinterpret_cast<T *>(smem);
+    T *ev = panel + PANEL;
+    int32_t *rp = reinterpret_cast<int32_t *>(ev + SA_EMAX);
+    uint16_t *ek = reinterpret_cast<uint16_t *>(rp + SA_ROWS + 1);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wrow = __builtin_amdgcn_readfirstlane(tid >> 6) * SA_R;   // local row base of this wave
+    // XCD-aware tile order: row blocks of one column block are consecutive logical tiles, and
+    // logical tiles are dealt XCD-contiguously, so they share the Y panel through one L2.
+    const int64_t nb = (int64_t)gridDim.x;
+    const int64_t b = blockIdx.x;
+    const int64_t xcd = b % 8, qq = nb / 8, rr = nb % 8;
+    const int64_t t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + b / 8;
+    const int64_t rb0 = (t % nrb) * SA_ROWS;
+    const int64_t j0 = (t / nrb) * SA_J;
+    const int nrows = (int)((p.M - rb0) < SA_ROWS ? (p.M - rb0) : SA_ROWS);
+    const int64_t j = j0 + lane;
+    const bool jin = j < p.N;
+    T *C = (T *)p.C;
+    const T beta = (T)p.beta;
+
+    T acc[SA_R];
+    {
+        const T *cb = C + (rb0 + wrow) * p.crs + j * p.ccs;   // element r at cb[r * crs]
+#pragma unroll
+        for (int r = 0; r < SA_R; ++r)
+            acc[r] = (beta != (T)0 && jin && rb0 + wrow + r < p.M) ? beta * cb[r * p.crs] : (T)0;
+    }
+
+    SaPrefetch<T, VP> f;
+    sa_load<T, VP>(f, p, vrp, kl, kv, 0, j0, rb0, nrows, tid);
+    for (int64_t c = 0; c < nchunks; ++c) {
         __syncthreads();
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int64_t i = rb0 + tid + r * SP_NT;
-        if (i >= p.M) continue;
-#pragma unroll
-        for (int c = 0; c < SP_J; ++c) {
-            const int64_t j = j0 + c;
-            if (j < p.N) C[i * p.crs + j * p.ccs] = acc[r][c];
+        sa_store<T, VP>(f, panel, ek, ev, rp, p, tid);
+        const int32_t ebase = f.ebase;
+        const int ecount = f.ecount;
+        __syncthreads();
+        if (c + 1 < nchunks && !(p.ablate & 2)) sa_load<T, VP>(f, p, vrp, kl, kv, c + 1, j0, rb0, nrows, tid);
+        if (!(p.ablate & 1)) sa_compute<T>(acc, panel, ek, ev, rp, 0, min(ecount, SA_EMAX), wrow, lane);
+        // rare: more entries in this chunk than LDS holds -> further windows, in order
+        for (int w = SA_EMAX; w < ecount; w += SA_EMAX) {
+            __syncthreads();
+            const int wn = min(ecount - w, SA_EMAX);
+            for (int e = tid; e < wn; e += SA_NT) {
+                ek[e] = kl[ebase + w + e];
+                ev[e] = kv[ebase + w + e];
+            }
+            __syncthreads();
+            sa_compute<T>(acc, panel, ek, ev, rp, w, w + wn, wrow, lane);
         }
     }
+    if (!jin) return;
+    // recompute the output base behind an opaque move so the prologue's per-row addresses are not
+    // kept live across the chunk loop
+    int64_t off = (rb0 + wrow) * p.crs + j * p.ccs;
+    asm volatile("" : "+v"(off));
+    T *cb = C + off;
+    const int64_t rem = p.M - (rb0 + wrow);   // rows of this wave that exist
+#pragma unroll
+    for (int r = 0; r < SA_R; ++r)
+        if (r < rem) cb[r * p.crs] = acc[r];
 }
 
 template <typename T>
 static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, const int64_t *cols, const T *vals,
                                      int64_t nnz, hipStream_t s) {
     if (p.M <= 0 || p.N <= 0) return hipSuccess;
+    if (nnz >= (int64_t)0x7fffffff) return hipErrorInvalidValue;
     hipError_t err;
-    // workspace
+    const int64_t nchunks = p.K > 0 ? (p.K + SP_KC - 1) / SP_KC : 0;
+    const int64_t NV = nchunks * p.M;
     const size_t n = (size_t)(nnz > 0 ? nnz : 1);
     size_t tmp_bytes = 0;
     uint64_t *k_in = nullptr, *k_out = nullptr;
     T *v_in = nullptr, *v_out = nullptr;
-    int64_t *rowptr = nullptr;
-    int32_t *kidx = nullptr;
+    int32_t *vrp = nullptr;
+    uint16_t *kl = nullptr;
     void *tmp = nullptr;
     int end_bit = 1;
     {
-        const unsigned long long maxkey = (unsigned long long)p.M * (unsigned long long)p.K;
+        const unsigned long long maxkey = (unsigned long long)(NV + 1) * SP_KC;
         while (end_bit < 64 && (1ull << end_bit) <= maxkey) ++end_bit;
     }
     err = rocprim::radix_sort_pairs(nullptr, tmp_bytes, k_in, k_out, v_in, v_out, n, 0, (unsigned)end_bit, s);
     if (err != hipSuccess) return err;
-    const size_t bytes = 2 * n * sizeof(uint64_t) + 2 * n * sizeof(T) + (size_t)(p.M + 1) * sizeof(int64_t) +
-                         n * sizeof(int32_t) + tmp_bytes + 256;
+    const size_t bytes = 2 * n * sizeof(uint64_t) + 2 * n * sizeof(T) + (size_t)(NV + 1) * sizeof(int32_t) +
+                         n * sizeof(uint16_t) + tmp_bytes + 256;
     char *ws = nullptr;
     err = hipMallocAsync((void **)&ws, bytes, s);
     if (err != hipSuccess) return err;
@@ -248,28 +382,26 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
     k_out = (uint64_t *)carve(n * sizeof(uint64_t));
     v_in = (T *)carve(n * sizeof(T));
     v_out = (T *)carve(n * sizeof(T));
-    rowptr = (int64_t *)carve((size_t)(p.M + 1) * sizeof(int64_t));
-    kidx = (int32_t *)carve(n * sizeof(int32_t));
+    vrp = (int32_t *)carve((size_t)(NV + 1) * sizeof(int32_t));
+    kl = (uint16_t *)carve(n * sizeof(uint16_t));
     tmp = carve(tmp_bytes);
 
     if (nnz > 0) {
         hipLaunchKernelGGL(coo_keys_kernel<T>, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, rows, cols,
-                           vals, p.ro, p.co, p.win_r, p.win_c, p.transposed, p.K, (T)p.alpha, k_in, v_in);
-        // invalid keys (~0) must still sort last: with end_bit < 64 their low bits are all ones,
-        // which is >= any valid key below 2^end_bit.
+                           vals, p.ro, p.co, p.win_r, p.win_c, p.transposed, p.M, (T)p.alpha, k_in, v_in);
+        // invalid keys (~0) still sort last: their low end_bit bits are all ones, above every valid key
         err = rocprim::radix_sort_pairs(tmp, tmp_bytes, k_in, k_out, v_in, v_out, (size_t)nnz, 0, (unsigned)end_bit, s);
         if (err != hipSuccess) { (void)hipFreeAsync(ws, s); return err; }
     }
-    hipLaunchKernelGGL(rowptr_kernel, dim3((unsigned)((nnz + 1 + 255) / 256)), dim3(256), 0, s, nnz, k_out, p.M,
-                       p.K, rowptr, kidx);
-    const unsigned gx = (unsigned)((p.N + SP_J - 1) / SP_J);
+    hipLaunchKernelGGL(rowptr_kernel, dim3((unsigned)((nnz + 1 + 255) / 256)), dim3(256), 0, s, nnz, k_out, NV, vrp,
+                       kl);
+    const int64_t nrb = (p.M + SA_ROWS - 1) / SA_ROWS;
+    const dim3 grid((unsigned)(((p.N + SA_J - 1) / SA_J) * nrb));
     timing_begin(s);
-    if (p.M <= SP_NT) {
-        hipLaunchKernelGGL((saso_apply_kernel<T, 1>), dim3(gx, 1), dim3(SP_NT), 0, s, p, rowptr, kidx, v_out);
-    } else {
-        const unsigned gy = (unsigned)((p.M + 2 * SP_NT - 1) / (2 * SP_NT));
-        hipLaunchKernelGGL((saso_apply_kernel<T, 2>), dim3(gx, gy), dim3(SP_NT), 0, s, p, rowptr, kidx, v_out);
-    }
+    const bool vecpanel = p.ysk == 1 && (p.ysj % PanelVec<T>::N) == 0 && (((uintptr_t)p.Y) % 16) == 0 &&
+                          (p.K % PanelVec<T>::N) == 0;
+    if (vecpanel) hipLaunchKernelGGL((saso_apply_kernel<T, true>), grid, dim3(SA_NT), 0, s, p, vrp, kl, v_out, nchunks, nrb);
+    else hipLaunchKernelGGL((saso_apply_kernel<T, false>), grid, dim3(SA_NT), 0, s, p, vrp, kl, v_out, nchunks, nrb);
     err = hipGetLastError();
     timing_end(s);
     hipError_t e2 = hipFreeAsync(ws, s);
