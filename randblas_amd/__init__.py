@@ -20,7 +20,7 @@ from typing import Optional
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librandblas_hip.so")
+LIB_PATH = os.environ.get("RBH_LIB_PATH") or os.path.join(_HERE, "librandblas_hip.so")   # override: kernel-variant experiments
 
 # One HIP runtime per process: torch ships its own libamdhip64 (soname libamdhip64.so.7). Loading
 # torch first makes this library bind to that same runtime instead of /opt/rocm's copy, so device

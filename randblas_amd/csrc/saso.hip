@@ -150,13 +150,31 @@ __global__ void rowptr_kernel(int64_t nnz, const uint64_t *keys, int64_t NV, int
 // The next chunk's panel, entries and row pointers are loaded into registers while the current
 // chunk is consumed. Each lane keeps its 32 running sums in registers across all chunks.
 // ------------------------------------------------------------------------------------------
+#ifndef SA_R_DEF
+#define SA_R_DEF 32
+#endif
+#ifndef SA_WPE_DEF
+#define SA_WPE_DEF 4
+#endif
+#ifndef SA_B_DEF
+#define SA_B_DEF 2
+#endif
+#ifndef SA_EMAX_DEF
+#define SA_EMAX_DEF 2048
+#endif
 constexpr int SA_NT = 1024;                  // threads per workgroup
 constexpr int SA_J = 64;                     // output columns per workgroup (one per lane)
-constexpr int SA_R = 32;                     // output rows per wave
-constexpr int SA_ROWS = SA_NT / 64 * SA_R;   // 512 output rows per workgroup
+constexpr int SA_R = SA_R_DEF;               // output rows per wave
+constexpr int SA_B = SA_B_DEF;                      // rows whose first entries are fetched together
+constexpr int SA_ROWS = SA_NT / 64 * SA_R;   // output rows per workgroup
 constexpr int SA_LDP = SP_KC + 1;            // panel column stride (elements)
-constexpr int SA_EMAX = 2048;                // entries staged in LDS per chunk (more: extra windows)
-constexpr int SA_ESLOT = SA_EMAX / SA_NT;    // entry prefetch slots per thread
+constexpr int SA_EMAX = SA_EMAX_DEF;         // entries staged in LDS per chunk (more: extra windows)
+constexpr int SA_ESLOT = (SA_EMAX + SA_NT - 1) / SA_NT;   // entry prefetch slots per thread
+static_assert(SA_R % SA_B == 0, "row batches");
+
+// A chunk entry as the apply reads it: value and byte offset of its k inside a panel column. One
+// broadcast LDS read fetches both.
+template <typename T> struct SaRec { T v; uint32_t koff; };
 
 template <typename T> struct PanelVec;
 template <> struct PanelVec<double> { typedef double v __attribute__((ext_vector_type(2))); static constexpr int N = 2; };
@@ -175,10 +193,21 @@ struct SaPrefetch {
     int32_t ebase, ecount;
 };
 
+// Entry range of chunk c's rows rb0 .. rb0+nrows in the CSR arrays: lane 0 loads its start, every
+// other lane its end. Kept as a per-lane value (so the compiler does not read it into a scalar,
+// and wait for it, right after the load); sa_range() extracts it one iteration later.
+__device__ __forceinline__ int sa_bounds(const SparseApply &p, const int32_t *vrp, int64_t c, int64_t rb0, int nrows,
+                                         int lane) {
+    return vrp[c * p.M + rb0 + (lane == 0 ? 0 : nrows)];
+}
+__device__ __forceinline__ int2 sa_range(int b) {
+    return make_int2(__builtin_amdgcn_readlane(b, 0), __builtin_amdgcn_readlane(b, 1));
+}
+
 template <typename T, bool VP>
 __device__ __forceinline__ void sa_load(SaPrefetch<T, VP> &f, const SparseApply &p, const int32_t *vrp,
                                         const uint16_t *kl, const T *kv, int64_t c, int64_t j0, int64_t rb0,
-                                        int nrows, int tid) {
+                                        int nrows, int tid, int2 bnd) {
     const T *Y = (const T *)p.Y;
     const int64_t kc0 = c * SP_KC;
     if (VP) {
@@ -205,11 +234,13 @@ __device__ __forceinline__ void sa_load(SaPrefetch<T, VP> &f, const SparseApply 
             f.ps[q] = (gk < p.K && gj < p.N) ? Y[gk * p.ysk + gj * p.ysj] : (T)0;
         }
     }
+    // the chunk's entry range was fetched one iteration earlier (sa_bounds), so nothing here waits
+    // on a load issued in this call and the panel loads stay in flight across the compute
     const int64_t v0 = c * p.M + rb0;
-    const int32_t base = vrp[v0];
+    const int32_t base = bnd.x;
     f.ebase = base;
-    f.ecount = vrp[v0 + nrows] - base;
-    f.rp0 = vrp[v0 + (tid < nrows ? tid : nrows)] - base;   // row pointers 0..nrows (rest: end)
+    f.ecount = bnd.y - base;
+    f.rp0 = vrp[v0 + (tid < nrows ? tid : nrows)];   // row pointers 0..nrows (rest: end), made relative at store
 #pragma unroll
     for (int q = 0; q < SA_ESLOT; ++q) {
         const int e = tid + q * SA_NT;
@@ -221,7 +252,7 @@ __device__ __forceinline__ void sa_load(SaPrefetch<T, VP> &f, const SparseApply 
 }
 
 template <typename T, bool VP>
-__device__ __forceinline__ void sa_store(const SaPrefetch<T, VP> &f, T *panel, uint16_t *ek, T *ev, int32_t *rp,
+__device__ __forceinline__ void sa_store(const SaPrefetch<T, VP> &f, T *panel, SaRec<T> *rec, int32_t *rp,
                                          const SparseApply &p, int tid) {
     if (VP) {
         constexpr int VEC = PanelVec<T>::N;
@@ -243,52 +274,75 @@ __device__ __forceinline__ void sa_store(const SaPrefetch<T, VP> &f, T *panel, u
             panel[cc * SA_LDP + kk] = f.ps[q];
         }
     }
-    if (tid <= SA_ROWS) rp[tid] = f.rp0;
+    if (tid <= SA_ROWS) rp[tid] = f.rp0 - f.ebase;
 #pragma unroll
     for (int q = 0; q < SA_ESLOT; ++q) {
         const int e = tid + q * SA_NT;
-        if (e < f.ecount && e < SA_EMAX) {
-            ek[e] = f.ek[q];
-            ev[e] = f.ev[q];
-        }
+        if (e < f.ecount && e < SA_EMAX) rec[e] = SaRec<T>{f.ev[q], (uint32_t)f.ek[q] * (uint32_t)sizeof(T)};
     }
 }
 
-// One chunk (or one window [wlo, whi) of its entries, held in LDS at e - wlo): the wave walks its
-// 32 rows; all bounds are wave-uniform (read once per lane, then readlane'd into scalars).
+// One chunk (or one window [wlo, whi) of its entries, held in LDS at e - wlo). The wave walks its
+// SA_R rows in batches of SA_B: the first entry of every row in a batch is fetched together (record
+// read, then panel read), so those reads overlap; a row's further entries follow in a plain loop.
+// All bounds are wave-uniform (row pointers read once per lane, then readlane'd into scalars).
 template <typename T>
-__device__ __forceinline__ void sa_compute(T (&acc)[SA_R], const T *panel, const uint16_t *ek, const T *ev,
+__device__ __forceinline__ void sa_compute(T (&acc)[SA_R], const char *pcol, const SaRec<T> *rec,
                                            const int32_t *rp, int wlo, int whi, int wrow, int lane) {
-    const T *pcol = panel + lane * SA_LDP;
-    const int myrp = rp[wrow + (lane < SA_R ? lane : SA_R)];   // this wave's 33 row pointers
+    const int myrp = rp[wrow + (lane < SA_R ? lane : SA_R)];   // this wave's SA_R + 1 row pointers
 #pragma unroll
-    for (int r = 0; r < SA_R; ++r) {
-        const int e0 = max(__builtin_amdgcn_readlane(myrp, r), wlo) - wlo;
-        const int e1 = min(__builtin_amdgcn_readlane(myrp, r + 1), whi) - wlo;
-        T s = acc[r];
-        for (int e = e0; e < e1; ++e) {
+    for (int rb = 0; rb < SA_R; rb += SA_B) {
+        int f[SA_B], n[SA_B];
+        SaRec<T> m[SA_B];
+        T y[SA_B];
+#pragma unroll
+        for (int q = 0; q < SA_B; ++q) {
+            const int a = max(__builtin_amdgcn_readlane(myrp, rb + q), wlo) - wlo;
+            const int b = min(__builtin_amdgcn_readlane(myrp, rb + q + 1), whi) - wlo;
+            f[q] = a;
+            n[q] = b - a;
+        }
+        // records past the window end are stale but hold valid offsets (rec is zeroed at start)
+#pragma unroll
+        for (int q = 0; q < SA_B; ++q) m[q] = rec[f[q]];
+#pragma unroll
+        for (int q = 0; q < SA_B; ++q) y[q] = *reinterpret_cast<const T *>(pcol + m[q].koff);
+#pragma unroll
+        for (int q = 0; q < SA_B; ++q) {
+            T s = acc[rb + q];
+            if (n[q] > 0) {
 #if defined(__clang__)
 #pragma clang fp contract(off)
 #endif
-            const T prod = ev[e] * pcol[ek[e]];
-            s = s + prod;
+                const T prod = m[q].v * y[q];
+                s = s + prod;
+            }
+            for (int e = f[q] + 1; e < f[q] + n[q]; ++e) {
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+                const SaRec<T> r = rec[e];
+                const T prod = r.v * *reinterpret_cast<const T *>(pcol + r.koff);
+                s = s + prod;
+            }
+            acc[rb + q] = s;
         }
-        acc[r] = s;
     }
 }
 
 template <typename T, bool VP>
-__global__ __launch_bounds__(SA_NT) void saso_apply_kernel(const SparseApply p, const int32_t *vrp, const uint16_t *kl,
-                                                            const T *kv, int64_t nchunks, int64_t nrb) {
-    // one LDS array, carved (panel | values | row pointers | u16 k)
+__global__ __launch_bounds__(SA_NT) __attribute__((amdgpu_waves_per_eu(SA_WPE_DEF))) void saso_apply_kernel(const SparseApply p, const int32_t *vrp,
+                                                                       const uint16_t *kl, const T *kv,
+                                                                       int64_t nchunks, int64_t nrb) {
+    // one LDS array, carved (panel | records | row pointers)
     constexpr int PANEL = SA_J * SA_LDP;
-    constexpr size_t BYTES = PANEL * sizeof(T) + SA_EMAX * sizeof(T) + (SA_ROWS + 1) * sizeof(int32_t) +
-                             SA_EMAX * sizeof(uint16_t);
+    constexpr int NREC = SA_EMAX + 1;
+    constexpr size_t PBYTES = ((PANEL * sizeof(T) + 15) / 16) * 16;
+    constexpr size_t BYTES = PBYTES + NREC * sizeof(SaRec<T>) + (SA_ROWS + 1) * sizeof(int32_t);
     __shared__ __attribute__((aligned(16))) char smem[BYTES];
     T *panel = reinterpret_cast<T *>(smem);
-    T *ev = panel + PANEL;
-    int32_t *rp = reinterpret_cast<int32_t *>(ev + SA_EMAX);
-    uint16_t *ek = reinterpret_cast<uint16_t *>(rp + SA_ROWS + 1);
+    SaRec<T> *rec = reinterpret_cast<SaRec<T> *>(smem + PBYTES);
+    int32_t *rp = reinterpret_cast<int32_t *>(rec + NREC);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -306,6 +360,9 @@ __global__ __launch_bounds__(SA_NT) void saso_apply_kernel(const SparseApply p, 
     const bool jin = j < p.N;
     T *C = (T *)p.C;
     const T beta = (T)p.beta;
+    const char *pcol = reinterpret_cast<const char *>(panel + lane * SA_LDP);
+
+    for (int e = tid; e < NREC; e += SA_NT) rec[e] = SaRec<T>{(T)0, 0u};
 
     T acc[SA_R];
     {
@@ -315,26 +372,30 @@ __global__ __launch_bounds__(SA_NT) void saso_apply_kernel(const SparseApply p, 
             acc[r] = (beta != (T)0 && jin && rb0 + wrow + r < p.M) ? beta * cb[r * p.crs] : (T)0;
     }
 
+    // software pipeline: chunk c in LDS, chunk c+1's data in registers, chunk c+2's entry range in
+    // flight
     SaPrefetch<T, VP> f;
-    sa_load<T, VP>(f, p, vrp, kl, kv, 0, j0, rb0, nrows, tid);
+    sa_load<T, VP>(f, p, vrp, kl, kv, 0, j0, rb0, nrows, tid, sa_range(sa_bounds(p, vrp, 0, rb0, nrows, lane)));
+    int bnext = sa_bounds(p, vrp, nchunks > 1 ? 1 : 0, rb0, nrows, lane);
     for (int64_t c = 0; c < nchunks; ++c) {
         __syncthreads();
-        sa_store<T, VP>(f, panel, ek, ev, rp, p, tid);
+        sa_store<T, VP>(f, panel, rec, rp, p, tid);
         const int32_t ebase = f.ebase;
         const int ecount = f.ecount;
         __syncthreads();
-        if (c + 1 < nchunks && !(p.ablate & 2)) sa_load<T, VP>(f, p, vrp, kl, kv, c + 1, j0, rb0, nrows, tid);
-        if (!(p.ablate & 1)) sa_compute<T>(acc, panel, ek, ev, rp, 0, min(ecount, SA_EMAX), wrow, lane);
+        if (c + 1 < nchunks && !(p.ablate & 2)) {
+            sa_load<T, VP>(f, p, vrp, kl, kv, c + 1, j0, rb0, nrows, tid, sa_range(bnext));
+            if (c + 2 < nchunks) bnext = sa_bounds(p, vrp, c + 2, rb0, nrows, lane);
+        }
+        if (!(p.ablate & 1)) sa_compute<T>(acc, pcol, rec, rp, 0, min(ecount, SA_EMAX), wrow, lane);
         // rare: more entries in this chunk than LDS holds -> further windows, in order
         for (int w = SA_EMAX; w < ecount; w += SA_EMAX) {
             __syncthreads();
             const int wn = min(ecount - w, SA_EMAX);
-            for (int e = tid; e < wn; e += SA_NT) {
-                ek[e] = kl[ebase + w + e];
-                ev[e] = kv[ebase + w + e];
-            }
+            for (int e = tid; e < wn; e += SA_NT)
+                rec[e] = SaRec<T>{kv[ebase + w + e], (uint32_t)kl[ebase + w + e] * (uint32_t)sizeof(T)};
             __syncthreads();
-            sa_compute<T>(acc, panel, ek, ev, rp, w, w + wn, wrow, lane);
+            sa_compute<T>(acc, pcol, rec, rp, w, w + wn, wrow, lane);
         }
     }
     if (!jin) return;
