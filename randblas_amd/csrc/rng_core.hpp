@@ -180,7 +180,9 @@ constexpr LogfEntry LOGF_TAB[16] = {
     {0x1.886e6037841edp-1, 0x1.1058bc8a07ee1p-2}, {0x1.767dcf5534862p-1, 0x1.4043057b6ee09p-2},
 };
 
-RB_HD float rb_logf(float xf) {
+// tab: LOGF_TAB or a copy of it (the fused GEMM keeps one in LDS, away from the vector-memory
+// counter its operand prefetch waits on).
+RB_HD float rb_logf_tab(float xf, const LogfEntry *tab) {
 #if defined(__clang__)
 #pragma clang fp contract(off)
 #endif
@@ -190,8 +192,8 @@ RB_HD float rb_logf(float xf) {
     const int i = (int)((tmp >> (23 - 4)) % 16);
     const int k = (int32_t)tmp >> 23;
     const uint32_t iz = ix - (tmp & (0x1ffu << 23));
-    const double invc = LOGF_TAB[i].invc;
-    const double logc = LOGF_TAB[i].logc;
+    const double invc = tab[i].invc;
+    const double logc = tab[i].logc;
     const double z = (double)f32_from(iz);
     const double r = RB_FMA(z, invc, -1.0);
     const double y0 = RB_FMA((double)k, LOGF_LN2, logc);
@@ -202,6 +204,7 @@ RB_HD float rb_logf(float xf) {
     const float res = (float)y;
     return (ix == 0x3f800000u) ? 0.0f : res;
 }
+RB_HD float rb_logf(float xf) { return rb_logf_tab(xf, LOGF_TAB); }
 
 // Correctly rounded float sqrt via double (double rounding is innocuous for sqrt at p = 53).
 RB_HD float rb_sqrtf(float v) {
@@ -213,14 +216,14 @@ RB_HD float rb_sqrtf(float v) {
 }
 
 // r123::boxmuller(u0, u1) -> {r*sin(pi*x), r*cos(pi*x)}, x = uneg11(u0), r = sqrt(-2 log u01(u1)).
-RB_HD void boxmuller(uint32_t u0, uint32_t u1, float &g0, float &g1) {
+RB_HD void boxmuller(uint32_t u0, uint32_t u1, float &g0, float &g1, const LogfEntry *tab = LOGF_TAB) {
 #if defined(__clang__)
 #pragma clang fp contract(off)
 #endif
     const float PIf = 3.1415926535897932f;
     float s, c;
     rb_sincosf(PIf * uneg11f(u0), s, c);
-    const float r = rb_sqrtf(-2.0f * rb_logf(u01f(u1)));
+    const float r = rb_sqrtf(-2.0f * rb_logf_tab(u01f(u1), tab));
     g0 = s * r;
     g1 = c * r;
 }
@@ -230,10 +233,10 @@ enum Family : int { GAUSSIAN = 0, UNIFORM = 1 };
 
 // The four float samples of one Philox call (r123ext::boxmul / r123ext::uneg11 generate()).
 template <int FAMILY>
-RB_HD void sample4(const u32x4 &w, float out[4]) {
+RB_HD void sample4(const u32x4 &w, float out[4], const LogfEntry *tab = LOGF_TAB) {
     if (FAMILY == GAUSSIAN) {
-        boxmuller(w.v[0], w.v[1], out[0], out[1]);
-        boxmuller(w.v[2], w.v[3], out[2], out[3]);
+        boxmuller(w.v[0], w.v[1], out[0], out[1], tab);
+        boxmuller(w.v[2], w.v[3], out[2], out[3], tab);
     } else {
         out[0] = uneg11f(w.v[0]); out[1] = uneg11f(w.v[1]);
         out[2] = uneg11f(w.v[2]); out[3] = uneg11f(w.v[3]);

@@ -24,6 +24,9 @@
 //     row tiles that share one Y column panel run on one XCD and share its L2.
 #include "common.hpp"
 
+#include <cstdlib>
+#include <type_traits>
+
 namespace rbh {
 
 constexpr int BK = 16;
@@ -51,12 +54,13 @@ template <> struct Mfma<float> {
 // Generated operand tile -> LDS
 // ------------------------------------------------------------------------------------------
 template <typename T, int FAMILY>
-__device__ __forceinline__ void gen_call(const GenOperand &g, uint64_t off, T out[4]) {
+__device__ __forceinline__ void gen_call(const GenOperand &g, uint64_t off, T out[4],
+                                         const rb::LogfEntry *tab = rb::LOGF_TAB) {
     uint32_t c[4];
     rb::ctr_add(g.ctr, off, c);
     const rb::u32x4 w = rb::philox4x32<10>(c[0], c[1], c[2], c[3], g.key[0], g.key[1]);
     float s[4];
-    rb::sample4<FAMILY>(w, s);
+    rb::sample4<FAMILY>(w, s, tab);
     if (FAMILY == rb::UNIFORM) {
         const T sc = (T)g.scale;
 #pragma unroll
@@ -112,6 +116,57 @@ __device__ __forceinline__ void gen_tile(const GenOperand &g, int64_t o0, int64_
     }
 }
 
+// Straight-line variant for the fused fast path: requires pc0 % 4 == 0, so every Philox call of a
+// step covers 4 in-tile elements and each thread makes exactly CPT calls, with no loop or branch
+// (bounds become selects). That keeps generation in the same basic block as the MFMAs, where the
+// scheduler interleaves the two (sched_group_barrier below).
+template <typename T, int KIND, int NO, int NT>
+struct GenTileFast {
+    static constexpr int CALLS = NO * BK / 4;
+    static_assert(CALLS % NT == 0, "whole calls per thread");
+    static constexpr int CPT = CALLS / NT;
+    T v[CPT][4];
+    template <int FAMILY>
+    __device__ __forceinline__ void gen(const GenOperand &g, int64_t o0, int64_t k0, int64_t nO, int64_t K, int tid,
+                                        const rb::LogfEntry *tab) {
+#pragma unroll
+        for (int u = 0; u < CPT; ++u) {
+            const int c = tid + u * NT;
+            if (KIND == GEN_OK) {
+                const int o = c / (BK / 4), q = c % (BK / 4);
+                gen_call<T, FAMILY>(g, (uint64_t)(g.pr0 + o0 + o) * g.stride + (uint64_t)((g.pc0 + k0) >> 2) + q,
+                                    v[u], tab);
+                const bool orow = (o0 + o) < nO;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[u][e] = (orow && k0 + 4 * q + e < K) ? v[u][e] : (T)0;
+            } else {
+                const int k = c / (NO / 4), q = c % (NO / 4);
+                gen_call<T, FAMILY>(g, (uint64_t)(g.pr0 + k0 + k) * g.stride + (uint64_t)((g.pc0 + o0) >> 2) + q,
+                                    v[u], tab);
+                const bool kin = (k0 + k) < K;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[u][e] = (kin && o0 + 4 * q + e < nO) ? v[u][e] : (T)0;
+            }
+        }
+    }
+    __device__ __forceinline__ void store(T *lds, int tid) const {
+        constexpr int LDK = Mfma<T>::LDK;
+#pragma unroll
+        for (int u = 0; u < CPT; ++u) {
+            const int c = tid + u * NT;
+            if (KIND == GEN_OK) {
+                const int o = c / (BK / 4), q = c % (BK / 4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) lds[o * LDK + 4 * q + e] = v[u][e];
+            } else {
+                const int k = c / (NO / 4), q = c % (NO / 4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) lds[(4 * q + e) * LDK + k] = v[u][e];
+            }
+        }
+    }
+};
+
 // ------------------------------------------------------------------------------------------
 // Memory operand tile: global -> registers (issued one step ahead) -> LDS
 // ------------------------------------------------------------------------------------------
@@ -126,6 +181,7 @@ struct MemTile {
     static constexpr int NV = EPT / VEC;
     typedef typename Vec2<T>::type v_t;
     T v[EPT];
+    uint32_t okm;   // load_fast: bit e = vector e in range
     // mode 2: 16-B loads along k (operand contiguous along k, 16-B aligned rows, K % VEC == 0)
     // mode 1: scalar loads, consecutive threads walk k; mode 0: scalar loads walking o.
     __device__ __forceinline__ void load(const MemOperand &m, int64_t o0, int64_t k0, int64_t nO, int64_t K,
@@ -154,6 +210,39 @@ struct MemTile {
             const int k = kfast ? idx % BK : idx / NO;
             const int64_t go = o0 + o, gk = k0 + k;
             v[e] = (go < nO && gk < K) ? p[go * m.so + gk * m.sk] : (T)0;
+        }
+    }
+    // mode-2 load without branches (fast path): out-of-range vectors read a clamped in-range
+    // address and are zeroed by selects
+    __device__ __forceinline__ void load_fast(const MemOperand &m, int64_t o0, int64_t k0, int64_t nO, int64_t K,
+                                              int tid) {
+        const T *p = (const T *)m.ptr;
+#pragma unroll
+        for (int e = 0; e < NV; ++e) {
+            const int idx = tid + e * NT;
+            const int o = idx / (BK / VEC);
+            const int k = (idx % (BK / VEC)) * VEC;
+            const int64_t go = o0 + o, gk = k0 + k;
+            okm = (okm & ~(1u << e)) | ((go < nO && gk < K) ? (1u << e) : 0u);
+            const int64_t co = go < nO ? go : nO - 1, ck = gk < K ? gk : K - VEC;
+            const v_t x = *reinterpret_cast<const v_t *>(p + co * m.so + ck);
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) v[e * VEC + q] = x[q];
+        }
+    }
+    // store of a load_fast tile: the out-of-range vectors are zeroed here, after the loads landed
+    __device__ __forceinline__ void store_fast(T *lds, int tid) const {
+        constexpr int LDK = Mfma<T>::LDK;
+#pragma unroll
+        for (int e = 0; e < NV; ++e) {
+            const int idx = tid + e * NT;
+            const int o = idx / (BK / VEC);
+            const int k = (idx % (BK / VEC)) * VEC;
+            const bool ok = (okm >> e) & 1u;
+            v_t x;
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) x[q] = ok ? v[e * VEC + q] : (T)0;
+            *reinterpret_cast<v_t *>(lds + o * LDK + k) = x;
         }
     }
     __device__ __forceinline__ void store(T *lds, int tid, int mode) const {
@@ -291,6 +380,126 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void skge_gemm_kernel(const
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Fused fast path: one basic block per K step
+// ------------------------------------------------------------------------------------------
+// Same tiling and LDS layout as skge_gemm_kernel, restricted to one generated operand with
+// pc0 % 4 == 0 and one memory operand with 16-B rows along k (mode 2), the shape of every
+// sketch_general call with the window starting on a Philox quad. Each K step is straight-line
+// code: the memory operand's next tile is fetched, the generated operand's next tile is drawn
+// (Philox + Box-Muller, all VALU), and the current tile's MFMAs run; the two waves of each SIMD
+// take the draw and the MFMAs in opposite order, so one feeds the matrix pipe while the other
+// computes samples. The logf table of the Box-Muller transform sits in LDS, so the only
+// vector-memory traffic in the loop is the operand prefetch.
+template <typename T, int XK, int YK, int FAMILY, int BM, int BN, int WAVES_M, int WAVES_N>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void skge_fused_kernel(const GemmProblem p) {
+    constexpr int NT = 64 * WAVES_M * WAVES_N;
+    constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
+    constexpr int FA = WM / 16, FB = WN / 16;
+    constexpr int LDK = Mfma<T>::LDK;
+    constexpr int XS = BM * LDK, YS = BN * LDK;
+    typedef typename Mfma<T>::v4 acc_t;
+    static_assert((XK == MEM) != (YK == MEM), "one generated and one memory operand");
+
+    __shared__ __attribute__((aligned(16))) T lds[2 * (XS + YS)];
+    __shared__ rb::LogfEntry tab[16];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave % WAVES_M, wn = wave / WAVES_M;
+    if (tid < 16) tab[tid] = rb::LOGF_TAB[tid];
+
+    const int64_t nTm = (p.M + BM - 1) / BM, nTn = (p.N + BN - 1) / BN;
+    const int64_t nb = nTm * nTn;
+    const int64_t b = blockIdx.x;
+    const int64_t xcd = b % 8, qq = nb / 8, rr = nb % 8;
+    const int64_t t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + b / 8;
+    const int64_t tm = t % nTm, tn = t / nTm;
+    const int64_t i0 = tm * BM, j0 = tn * BN;
+
+    MemTile<T, (XK == MEM ? BM : BN), NT> mt;
+    GenTileFast<T, (XK == MEM ? YK : XK), (XK == MEM ? BN : BM), NT> gt;
+    const MemOperand &mo = XK == MEM ? p.xm : p.ym;
+    const GenOperand &go = XK == MEM ? p.yg : p.xg;
+    const int64_t mo0 = XK == MEM ? i0 : j0, go0 = XK == MEM ? j0 : i0;
+    const int64_t mnO = XK == MEM ? p.M : p.N, gnO = XK == MEM ? p.N : p.M;
+    const int moff = XK == MEM ? 0 : XS, goff = XK == MEM ? XS : 0;
+
+    acc_t acc[FA][FB];
+#pragma unroll
+    for (int a = 0; a < FA; ++a)
+#pragma unroll
+        for (int c = 0; c < FB; ++c) acc[a][c] = (acc_t){0, 0, 0, 0};
+
+    const int64_t nk = (p.K + BK - 1) / BK;
+    __syncthreads();   // tab
+    mt.load_fast(mo, mo0, 0, mnO, p.K, tid);
+    gt.template gen<FAMILY>(go, go0, 0, gnO, p.K, tid, tab);
+    mt.store_fast(lds + moff, tid);
+    gt.store(lds + goff, tid);
+    __syncthreads();
+
+    const int g4 = (lane >> 4) * 4;
+    const int r = lane & 15;
+
+    // The two waves sharing a SIMD (waves w and w + 4) run the step's two phases in opposite
+    // order -- one does its MFMAs while the other draws the next tile's samples -- so the matrix
+    // pipe of the SIMD is fed while the VALU works on the draw.
+    // (Two copies of the whole loop rather than a branch inside it: register allocation then sees
+    // one phase order per loop.)
+    auto k_loop = [&](auto mfma_first_tag) {
+        constexpr bool MFMA_FIRST = decltype(mfma_first_tag)::value;
+        for (int64_t kt = 0; kt < nk; ++kt) {
+            const int cur = (int)(kt & 1);
+            const T *Xc = lds + cur * (XS + YS);
+            const T *Yc = Xc + XS;
+            T *nxt = lds + (cur ^ 1) * (XS + YS);
+            // next step's operands (past K on the last step: clamped loads, zero samples, unused)
+            const int64_t kn = (kt + 1) * BK;
+            mt.load_fast(mo, mo0, kn, mnO, p.K, tid);
+            if (!MFMA_FIRST) gt.template gen<FAMILY>(go, go0, kn, gnO, p.K, tid, tab);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                T xf[FA], yf[FB];
+#pragma unroll
+                for (int a = 0; a < FA; ++a) xf[a] = Xc[(wm * WM + 16 * a + r) * LDK + g4 + s];
+#pragma unroll
+                for (int c = 0; c < FB; ++c) yf[c] = Yc[(wn * WN + 16 * c + r) * LDK + g4 + s];
+#pragma unroll
+                for (int a = 0; a < FA; ++a)
+#pragma unroll
+                    for (int c = 0; c < FB; ++c) acc[a][c] = Mfma<T>::mma(yf[c], xf[a], acc[a][c]);
+            }
+            if (MFMA_FIRST) gt.template gen<FAMILY>(go, go0, kn, gnO, p.K, tid, tab);
+            mt.store_fast(nxt + moff, tid);
+            gt.store(nxt + goff, tid);
+            __syncthreads();
+        }
+    };
+    if (__builtin_amdgcn_readfirstlane(wave) < 4) k_loop(std::true_type{});
+    else k_loop(std::false_type{});
+
+    T *C = (T *)p.C;
+    const T alpha = (T)p.alpha, beta = (T)p.beta;
+#pragma unroll
+    for (int a = 0; a < FA; ++a) {
+        const int64_t i = i0 + wm * WM + 16 * a + r;
+#pragma unroll
+        for (int c = 0; c < FB; ++c) {
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                const int64_t j = j0 + wn * WN + 16 * c + Mfma<T>::drow(lane, reg);
+                if (i < p.M && j < p.N) {
+                    T *dst = C + i + j * p.ldc;
+                    const T v = alpha * acc[a][c][reg];
+                    *dst = (beta == (T)0) ? v : v + beta * *dst;
+                }
+            }
+        }
+    }
+}
+
 template <typename T>
 __global__ void scale_kernel(int64_t M, int64_t N, T beta, T *C, int64_t ldc) {
     const int64_t total = M * N;
@@ -316,9 +525,42 @@ static hipError_t launch_one(const GemmProblem &p, hipStream_t s) {
     return e;
 }
 
+template <typename T, int XK, int YK, int FAMILY, int BM, int BN, int WMS, int WNS>
+static hipError_t launch_fused(const GemmProblem &p, hipStream_t s) {
+    const int64_t nb = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+    if (nb <= 0) return hipSuccess;
+    timing_begin(s);
+    hipLaunchKernelGGL((skge_fused_kernel<T, XK, YK, FAMILY, BM, BN, WMS, WNS>), dim3((unsigned)nb),
+                       dim3(64 * WMS * WNS), 0, s, p);
+    hipError_t e = hipGetLastError();
+    timing_end(s);
+    return e;
+}
+
+// The fused fast path applies when the generated window starts on a Philox quad and the memory
+// operand takes 16-B loads along k (see skge_fused_kernel); RBH_NO_FUSED=1 forces the generic kernel.
+static bool fused_ok(const GemmProblem &p) {
+    static const bool off = [] { const char *e = getenv("RBH_NO_FUSED"); return e && e[0] == '1'; }();
+    if (off) return false;
+    if ((p.xkind == MEM) == (p.ykind == MEM)) return false;
+    const GenOperand &g = p.xkind == MEM ? p.yg : p.xg;
+    const int mode = p.xkind == MEM ? p.xmode : p.ymode;
+    return mode == 2 && (g.pc0 & 3) == 0;
+}
+
 template <typename T>
 static hipError_t launch_gemm(const GemmProblem &p, hipStream_t s) {
     const bool unif = (p.xkind != MEM ? p.xg.family : p.yg.family) == rb::UNIFORM;
+    if (fused_ok(p)) {
+#define RBH_FUSED(XK, YK, BM, BN, WMS, WNS)                                                    \
+    return unif ? launch_fused<T, XK, YK, rb::UNIFORM, BM, BN, WMS, WNS>(p, s)                  \
+                : launch_fused<T, XK, YK, rb::GAUSSIAN, BM, BN, WMS, WNS>(p, s)
+        if (p.xkind == GEN_OK) { RBH_FUSED(GEN_OK, MEM, 128, 256, 2, 4); }
+        if (p.xkind == GEN_OO) { RBH_FUSED(GEN_OO, MEM, 128, 256, 2, 4); }
+        if (p.ykind == GEN_OK) { RBH_FUSED(MEM, GEN_OK, 256, 128, 4, 2); }
+        if (p.ykind == GEN_OO) { RBH_FUSED(MEM, GEN_OO, 256, 128, 4, 2); }
+#undef RBH_FUSED
+    }
 #define RBH_FAM(XK, YK, BM, BN, WMS, WNS)                                                    \
     return unif ? launch_one<T, XK, YK, rb::UNIFORM, BM, BN, WMS, WNS>(p, s)                  \
                 : launch_one<T, XK, YK, rb::GAUSSIAN, BM, BN, WMS, WNS>(p, s)
