@@ -46,6 +46,25 @@ CONFIGS = {
 }
 
 
+def pmc_traffic(config):
+    """HBM bytes per launch of the dominant kernel, from the committed rocprofv3 PMC summary of this
+    config (tools/pmc.sh -> tools/pmc_summary.py -> profiles/<round>/<config>_pmc.json): FETCH_SIZE
+    (doubled, the gfx950 correction of MI355X_MICROARCH.md) + WRITE_SIZE. The dominant kernel is the
+    one with the most GRBM_GUI_ACTIVE cycles. None when no summary exists."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r*",
+                                          f"{config}_pmc.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    kern = max(d, key=lambda k: d[k].get("GRBM_GUI_ACTIVE", 0.0))
+    if "hbm_bytes" not in d[kern]:
+        return None, None
+    rel = os.path.relpath(files[-1], os.path.dirname(os.path.abspath(__file__)))
+    return d[kern]["hbm_bytes"], f"{rel}: {kern}"
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -202,6 +221,9 @@ def main():
         achieved = flops / (kern_ms * 1e-3)
         roof = {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK[dtype] / 1e12, "unit": "TFLOP/s",
                 "frac": achieved / PEAK[dtype], "traffic": None}
+
+    if world == 1:
+        roof["traffic"], roof["traffic_source"] = pmc_traffic(args.config)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -123,19 +123,26 @@ __device__ __forceinline__ void gen_tile(const GenOperand &g, int64_t o0, int64_
 template <typename T, int KIND, int NO, int NT>
 struct GenTileFast {
     static constexpr int CALLS = NO * BK / 4;
-    static_assert(CALLS % NT == 0, "whole calls per thread");
-    static constexpr int CPT = CALLS / NT;
+    static_assert(CALLS % NT == 0 || (NT % CALLS == 0 && CALLS % 64 == 0), "whole calls per thread or per wave");
+    static constexpr int CPT = CALLS >= NT ? CALLS / NT : 1;
+    // fewer calls than threads: the first CALLS threads (whole waves) draw, the rest skip
+    __device__ static bool active(int tid) { return CALLS >= NT || tid < CALLS; }
     T v[CPT][4];
     template <int FAMILY>
     __device__ __forceinline__ void gen(const GenOperand &g, int64_t o0, int64_t k0, int64_t nO, int64_t K, int tid,
                                         const rb::LogfEntry *tab) {
+        if (!active(tid)) return;
 #pragma unroll
         for (int u = 0; u < CPT; ++u) {
             const int c = tid + u * NT;
             if (KIND == GEN_OK) {
                 const int o = c / (BK / 4), q = c % (BK / 4);
+#ifdef RBH_ABLATE_GEN
+                for (int e = 0; e < 4; ++e) v[u][e] = (T)(int)((o0 + o + k0 + q + e) & 7);   // diagnostics only
+#else
                 gen_call<T, FAMILY>(g, (uint64_t)(g.pr0 + o0 + o) * g.stride + (uint64_t)((g.pc0 + k0) >> 2) + q,
                                     v[u], tab);
+#endif
                 const bool orow = (o0 + o) < nO;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) v[u][e] = (orow && k0 + 4 * q + e < K) ? v[u][e] : (T)0;
@@ -149,8 +156,9 @@ struct GenTileFast {
             }
         }
     }
+    template <int LDK>
     __device__ __forceinline__ void store(T *lds, int tid) const {
-        constexpr int LDK = Mfma<T>::LDK;
+        if (!active(tid)) return;
 #pragma unroll
         for (int u = 0; u < CPT; ++u) {
             const int c = tid + u * NT;
@@ -231,8 +239,8 @@ struct MemTile {
         }
     }
     // store of a load_fast tile: the out-of-range vectors are zeroed here, after the loads landed
+    template <int LDK>
     __device__ __forceinline__ void store_fast(T *lds, int tid) const {
-        constexpr int LDK = Mfma<T>::LDK;
 #pragma unroll
         for (int e = 0; e < NV; ++e) {
             const int idx = tid + e * NT;
@@ -242,7 +250,12 @@ struct MemTile {
             v_t x;
 #pragma unroll
             for (int q = 0; q < VEC; ++q) x[q] = ok ? v[e * VEC + q] : (T)0;
-            *reinterpret_cast<v_t *>(lds + o * LDK + k) = x;
+            if constexpr ((LDK * sizeof(T)) % 16 == 0) {
+                *reinterpret_cast<v_t *>(lds + o * LDK + k) = x;
+            } else {   // rows not 16-B aligned: element stores (ds_write2)
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) lds[o * LDK + k + q] = x[q];
+            }
         }
     }
     __device__ __forceinline__ void store(T *lds, int tid, int mode) const {
@@ -391,12 +404,11 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void skge_gemm_kernel(const
 // take the draw and the MFMAs in opposite order, so one feeds the matrix pipe while the other
 // computes samples. The logf table of the Box-Muller transform sits in LDS, so the only
 // vector-memory traffic in the loop is the operand prefetch.
-template <typename T, int XK, int YK, int FAMILY, int BM, int BN, int WAVES_M, int WAVES_N>
+template <typename T, int XK, int YK, int FAMILY, int BM, int BN, int WAVES_M, int WAVES_N, int LDK>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void skge_fused_kernel(const GemmProblem p) {
     constexpr int NT = 64 * WAVES_M * WAVES_N;
     constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
     constexpr int FA = WM / 16, FB = WN / 16;
-    constexpr int LDK = Mfma<T>::LDK;
     constexpr int XS = BM * LDK, YS = BN * LDK;
     typedef typename Mfma<T>::v4 acc_t;
     static_assert((XK == MEM) != (YK == MEM), "one generated and one memory operand");
@@ -436,8 +448,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void skge_fused_kernel(cons
     __syncthreads();   // tab
     mt.load_fast(mo, mo0, 0, mnO, p.K, tid);
     gt.template gen<FAMILY>(go, go0, 0, gnO, p.K, tid, tab);
-    mt.store_fast(lds + moff, tid);
-    gt.store(lds + goff, tid);
+    mt.template store_fast<LDK>(lds + moff, tid);
+    gt.template store<LDK>(lds + goff, tid);
     __syncthreads();
 
     const int g4 = (lane >> 4) * 4;
@@ -472,8 +484,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void skge_fused_kernel(cons
                     for (int c = 0; c < FB; ++c) acc[a][c] = Mfma<T>::mma(yf[c], xf[a], acc[a][c]);
             }
             if (MFMA_FIRST) gt.template gen<FAMILY>(go, go0, kn, gnO, p.K, tid, tab);
-            mt.store_fast(nxt + moff, tid);
-            gt.store(nxt + goff, tid);
+            mt.template store_fast<LDK>(nxt + moff, tid);
+            gt.template store<LDK>(nxt + goff, tid);
             __syncthreads();
         }
     };
@@ -495,6 +507,233 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void skge_fused_kernel(cons
                     const T v = alpha * acc[a][c][reg];
                     *dst = (beta == (T)0) ? v : v + beta * *dst;
                 }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// f64 wide tile: 64 generated x 512 memory outer indices, memory operand by LDS-DMA
+// ------------------------------------------------------------------------------------------
+// With f64 MFMAs the draw's VALU work does not hide under the matrix pipe, so what the draw costs
+// is set by how often each operator entry is regenerated: once per tile along the memory
+// operand's outer dimension. A 64 x 512 tile draws each entry half as often as 128 x 256 for the
+// same accumulator budget (128 VGPRs per lane). The 512-row memory tile (64 KB per K step) would
+// need 32 staging VGPRs per lane, so it is copied global -> LDS with global_load_lds_dwordx4
+// instead: rows of 16 doubles, unpadded, 16-B vectors XOR-swizzled by (row >> 1) & 7 through the
+// source address, which leaves the fragment reads 2-way banked (the minimum for 128-B rows).
+// Waves 0-3 draw the 64 x 16 generated tile (one Philox call per lane) into padded LDS rows; waves
+// w and w + 4 share a SIMD, so every SIMD carries one drawing wave.
+// Requires K % 16 == 0, a mode-2 memory operand and pc0 % 4 == 0.
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+
+#ifndef RBH_WIDE_WG
+#define RBH_WIDE_WG 1
+#endif
+template <int GK, int FAMILY, bool GX>
+__global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
+    typedef double T;
+    // 8 waves = WGW (along the generated dimension) x WMW (along the memory dimension); each wave
+    // holds FA x FB MFMA tiles of 16 x 16 (FA * FB = 16: 128 accumulator VGPRs)
+    constexpr int WGW = RBH_WIDE_WG, WMW = 8 / WGW;
+    constexpr int BG = 64, BMM = 512;
+    constexpr int FA = BG / 16 / WGW, FB = BMM / 16 / WMW;
+    constexpr int LDG = BK + 2;
+    constexpr int GS = BG * LDG, MS = BMM * BK;
+    typedef Mfma<T>::v4 acc_t;
+
+    __shared__ __attribute__((aligned(16))) T lds[2 * MS + 2 * GS];   // [mem 0 | mem 1 | gen 0 | gen 1]
+    __shared__ rb::LogfEntry tab[16];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, r = lane & 15;
+    const int wg = wave % WGW, wmm = wave / WGW;
+    if (tid < 16) tab[tid] = rb::LOGF_TAB[tid];
+
+    const GenOperand &gop = GX ? p.xg : p.yg;
+    const MemOperand &mop = GX ? p.ym : p.xm;
+    const int64_t gnO = GX ? p.M : p.N, mnO = GX ? p.N : p.M;
+    const int64_t nTg = (gnO + BG - 1) / BG, nTm = (mnO + BMM - 1) / BMM;
+    const int64_t nb = nTg * nTm;
+    const int64_t b = blockIdx.x;
+    const int64_t xcd = b % 8, qq = nb / 8, rr = nb % 8;
+    const int64_t t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + b / 8;
+    const int64_t go0 = (t % nTg) * BG, mo0 = (t / nTg) * BMM;
+
+    // LDS-DMA of the memory tile for step k0 into stage st: this wave's 8 pieces of 8 rows
+    const T *mptr = (const T *)mop.ptr;
+    const int drow = lane >> 3, dslot = lane & 7;
+    auto dma = [&](int64_t k0, int st) {
+        const int64_t ck0 = k0 < p.K ? k0 : p.K - BK;   // past K (last step's prefetch): any valid address
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int blk = 8 * wave + i;
+            const int o = 8 * blk + drow;
+            const int v = dslot ^ ((o >> 1) & 7);
+            int64_t go = mo0 + o;
+            go = go < mnO ? go : mnO - 1;
+            const T *src = mptr + go * mop.so + ck0 + 2 * v;
+            __builtin_amdgcn_global_load_lds((glb_void_t *)src, (lds_void_t *)(lds + st * MS + blk * 128), 16, 0, 0);
+        }
+    };
+    // register staging (default; RBH_WIDE_DMA selects the LDS-DMA above): the same swizzled image,
+    // written with ds_write_b128 from two 4-vector halves, the second half loaded mid-step.
+    // Thread tid stages vectors idx = tid + 512 * e (e < 8): row o = (tid >> 3) + 64 * e, 16-B
+    // vector v = tid & 7, LDS slot v ^ ((o >> 1) & 7) = v ^ ((tid >> 4) & 7), the same for every e.
+    // Everything per lane is loop-invariant: per step only the uniform k offset moves (SGPR base
+    // + 32-bit VGPR offset addressing), so the staging costs no VALU in the loop.
+    typedef typename Vec2<T>::type v2_t;
+    v2_t rs[4];
+    const char *mtile = (const char *)(mptr + mo0 * mop.so);
+    // byte offset of vector e = voff0 + e * vstep, clamped to the last row of the operand
+    const uint32_t vstep = (uint32_t)(64 * mop.so * (int64_t)sizeof(T));
+    const uint32_t voff0 = (uint32_t)(((tid >> 3) * mop.so + 2 * (tid & 7)) * (int64_t)sizeof(T));
+    const uint32_t vmax = (uint32_t)(((mnO - 1 - mo0) * mop.so + 2 * (tid & 7)) * (int64_t)sizeof(T));
+    const int lwoff = (tid >> 3) * BK + 2 * ((tid & 7) ^ ((tid >> 4) & 7));   // doubles, + 1024 * e
+    auto rload = [&](int64_t k0, int half) {
+        const int64_t ck0 = k0 < p.K ? k0 : p.K - BK;
+        const char *base = mtile + ck0 * (int64_t)sizeof(T);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const uint32_t vo = voff0 + (uint32_t)(4 * half + e) * vstep;
+            rs[e] = *reinterpret_cast<const v2_t *>(base + (vo < vmax ? vo : vmax));
+        }
+    };
+    auto rstore = [&](int st, int half) {
+        T *dst = lds + st * MS + lwoff;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) *reinterpret_cast<v2_t *>(dst + 1024 * (4 * half + e)) = rs[e];
+    };
+    // draw of the 64 x 16 generated tile for step kt (waves 0-3, one Philox call per lane). (A
+    // counter precomputed per lane, advanced by a uniform step, saves a few VALU but costs the
+    // 4 VGPRs this kernel does not have.)
+    T gv[4];
+    const bool glane_ok = GK == GEN_OK ? go0 + (tid >> 2) < gnO : true;
+    const bool gtile_full = go0 + BG <= gnO;
+    auto draw = [&](int64_t kt) {
+        uint32_t c[4];
+        {
+            uint64_t off;
+            if (GK == GEN_OK) {
+                const int o = tid >> 2, q = tid & 3;
+                off = (uint64_t)(gop.pr0 + go0 + o) * gop.stride + (uint64_t)(gop.pc0 >> 2) + q + (uint64_t)kt * (BK / 4);
+            } else {
+                const int k = tid >> 4, q = tid & 15;
+                off = (uint64_t)(gop.pr0 + kt * BK + k) * gop.stride + (uint64_t)((gop.pc0 + go0) >> 2) + q;
+            }
+            rb::ctr_add(gop.ctr, off, c);
+        }
+#ifdef RBH_ABLATE_GEN
+        for (int e = 0; e < 4; ++e) gv[e] = (T)(int)((c[0] + e) & 7);   // diagnostics only
+#else
+        const rb::u32x4 w = rb::philox4x32<10>(c[0], c[1], c[2], c[3], gop.key[0], gop.key[1]);
+        float sm[4];
+        rb::sample4<FAMILY>(w, sm, tab);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) gv[e] = FAMILY == rb::UNIFORM ? (T)sm[e] * (T)gop.scale : (T)sm[e];
+#endif
+        if (!gtile_full || kt * BK >= p.K) {   // uniform: edge tile or the prefetch past K
+            if (GK == GEN_OK) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) gv[e] = (glane_ok && kt * BK < p.K) ? gv[e] : (T)0;
+            } else {
+                const int q = tid & 15;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) gv[e] = (go0 + 4 * q + e < gnO && kt * BK < p.K) ? gv[e] : (T)0;
+            }
+        }
+    };
+    auto gstore = [&](int st) {
+        T *G = lds + 2 * MS + st * GS;
+        if (GK == GEN_OK) {
+            const int o = tid >> 2, q = tid & 3;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) G[o * LDG + 4 * q + e] = gv[e];
+        } else {
+            const int k = tid >> 4, q = tid & 15;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) G[(4 * q + e) * LDG + k] = gv[e];
+        }
+    };
+
+    acc_t acc[FA][FB];
+#pragma unroll
+    for (int a = 0; a < FA; ++a)
+#pragma unroll
+        for (int c = 0; c < FB; ++c) acc[a][c] = (acc_t){0, 0, 0, 0};
+
+    const int64_t nk = p.K / BK;
+    __syncthreads();   // tab
+#ifndef RBH_WIDE_DMA
+    rload(0, 0); rstore(0, 0); rload(0, 1); rstore(0, 1);
+#else
+    dma(0, 0);
+#endif
+    if (wave < 4) { draw(0); gstore(0); }
+    __syncthreads();
+
+    // fragment addresses (doubles) relative to the stage base
+    const int gfa = (16 * FA * wg + r) * LDG + 4 * g;   // + 16 * a * LDG per fragment a
+    const int mrow = (16 * FB * wmm + r) * BK;          // + 16 * c * BK per fragment c
+    const int msw = (r >> 1) & 7;
+    for (int64_t kt = 0; kt < nk; ++kt) {
+        const int cur = (int)(kt & 1);
+        const T *Mc = lds + cur * MS;
+        const T *Gc = lds + 2 * MS + cur * GS;
+        const int64_t kn = (kt + 1) * BK;
+#ifndef RBH_WIDE_DMA
+        rload(kn, 0);
+#else
+        dma(kn, cur ^ 1);
+#endif
+        if (wave < 4) draw(kt + 1);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+#ifndef RBH_WIDE_DMA
+            if (s == 2) { rstore(cur ^ 1, 0); rload(kn, 1); }
+#endif
+            T gf[FA];
+#pragma unroll
+            for (int a = 0; a < FA; ++a) gf[a] = Gc[gfa + 16 * a * LDG + s];
+            const int moff = 2 * (((4 * g + s) >> 1) ^ msw) + (s & 1);
+            T mf[FB];
+#pragma unroll
+            for (int c = 0; c < FB; ++c) mf[c] = Mc[mrow + 16 * c * BK + moff];
+#pragma unroll
+            for (int a = 0; a < FA; ++a)
+#pragma unroll
+                for (int c = 0; c < FB; ++c)
+                    acc[a][c] = GX ? Mfma<T>::mma(mf[c], gf[a], acc[a][c]) : Mfma<T>::mma(gf[a], mf[c], acc[a][c]);
+#ifdef RBH_WIDE_SB
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+        }
+        if (wave < 4) gstore(cur ^ 1);
+#ifndef RBH_WIDE_DMA
+        rstore(cur ^ 1, 1);
+#endif
+        __syncthreads();
+    }
+
+    T *C = (T *)p.C;
+    const T alpha = (T)p.alpha, beta = (T)p.beta;
+#pragma unroll
+    for (int a = 0; a < FA; ++a)
+#pragma unroll
+    for (int c = 0; c < FB; ++c) {
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+            const int dr = Mfma<T>::drow(lane, reg);
+            const int64_t gi = go0 + 16 * FA * wg + 16 * a, mi = mo0 + 16 * FB * wmm + 16 * c;
+            const int64_t i = GX ? gi + r : mi + r;
+            const int64_t j = GX ? mi + dr : gi + dr;
+            if (i < p.M && j < p.N) {
+                T *dst = C + i + j * p.ldc;
+                const T v = alpha * acc[a][c][reg];
+                *dst = (beta == (T)0) ? v : v + beta * *dst;
             }
         }
     }
@@ -529,8 +768,10 @@ template <typename T, int XK, int YK, int FAMILY, int BM, int BN, int WMS, int W
 static hipError_t launch_fused(const GemmProblem &p, hipStream_t s) {
     const int64_t nb = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
     if (nb <= 0) return hipSuccess;
+    // two LDS stages of (BM + BN) rows: 17-element f64 rows keep the 64 x 512 tile under 160 KB
+    constexpr int LDK = (sizeof(T) == 8 && BM + BN > 384) ? BK + 1 : Mfma<T>::LDK;
     timing_begin(s);
-    hipLaunchKernelGGL((skge_fused_kernel<T, XK, YK, FAMILY, BM, BN, WMS, WNS>), dim3((unsigned)nb),
+    hipLaunchKernelGGL((skge_fused_kernel<T, XK, YK, FAMILY, BM, BN, WMS, WNS, LDK>), dim3((unsigned)nb),
                        dim3(64 * WMS * WNS), 0, s, p);
     hipError_t e = hipGetLastError();
     timing_end(s);
@@ -548,9 +789,36 @@ static bool fused_ok(const GemmProblem &p) {
     return mode == 2 && (g.pc0 & 3) == 0;
 }
 
+template <int GK, int FAMILY, bool GX>
+static hipError_t launch_wide(const GemmProblem &p, hipStream_t s) {
+    const int64_t gnO = GX ? p.M : p.N, mnO = GX ? p.N : p.M;
+    const int64_t nb = ((gnO + 63) / 64) * ((mnO + 511) / 512);
+    if (nb <= 0) return hipSuccess;
+    timing_begin(s);
+    hipLaunchKernelGGL((skge_wide_kernel<GK, FAMILY, GX>), dim3((unsigned)nb), dim3(512), 0, s, p);
+    hipError_t e = hipGetLastError();
+    timing_end(s);
+    return e;
+}
+
+template <typename T>
+static bool wide_ok(const GemmProblem &p) {
+    static const bool off = [] { const char *e = getenv("RBH_NO_WIDE"); return e && e[0] == '1'; }();
+    return sizeof(T) == 8 && !off && fused_ok(p) && p.K % BK == 0;
+}
+
 template <typename T>
 static hipError_t launch_gemm(const GemmProblem &p, hipStream_t s) {
     const bool unif = (p.xkind != MEM ? p.xg.family : p.yg.family) == rb::UNIFORM;
+    if (wide_ok<T>(p)) {
+#define RBH_WIDE_L(GK, GX)                                                                     \
+    return unif ? launch_wide<GK, rb::UNIFORM, GX>(p, s) : launch_wide<GK, rb::GAUSSIAN, GX>(p, s)
+        if (p.xkind == GEN_OK) { RBH_WIDE_L(GEN_OK, true); }
+        if (p.xkind == GEN_OO) { RBH_WIDE_L(GEN_OO, true); }
+        if (p.ykind == GEN_OK) { RBH_WIDE_L(GEN_OK, false); }
+        if (p.ykind == GEN_OO) { RBH_WIDE_L(GEN_OO, false); }
+#undef RBH_WIDE_L
+    }
     if (fused_ok(p)) {
 #define RBH_FUSED(XK, YK, BM, BN, WMS, WNS)                                                    \
     return unif ? launch_fused<T, XK, YK, rb::UNIFORM, BM, BN, WMS, WNS>(p, s)                  \
