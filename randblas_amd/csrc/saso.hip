@@ -110,10 +110,15 @@ hipError_t launch_fill_sparse_f32(const SparseGen &g, int64_t *rows, int64_t *co
 // ------------------------------------------------------------------------------------------
 constexpr int SP_KC = 128;        // contracted indices per chunk (LDS panel depth)
 
+// Magnitude test for the uniform-value apply (section 4): UniformTest.mixed is set unless every
+// in-window value alpha*v has the magnitude c = |alpha*vals[0]| (finite, nonzero), which holds for
+// every sampled SASO/LASO (values +-1). c is recorded for the apply's panel prescale.
+template <typename T> struct UniformTest { uint32_t mixed; uint32_t pad; T c; };
+
 template <typename T>
 __global__ void coo_keys_kernel(int64_t nnz, const int64_t *rows, const int64_t *cols, const T *vals, int64_t ro,
                                 int64_t co, int64_t win_r, int64_t win_c, int transposed, int64_t M, T alpha,
-                                uint64_t *keys, T *kv) {
+                                uint64_t *keys, T *kv, UniformTest<T> *ut) {
     const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (e >= nnz) return;
     const int64_t wr = rows[e] - ro, wc = cols[e] - co;
@@ -122,18 +127,35 @@ __global__ void coo_keys_kernel(int64_t nnz, const int64_t *rows, const int64_t 
     const uint64_t k = (uint64_t)(transposed ? wr : wc);
     const uint64_t v = (k / SP_KC) * (uint64_t)M + i;
     keys[e] = in ? v * SP_KC + (k % SP_KC) : ~(uint64_t)0;
-    kv[e] = alpha * vals[e];
+    const T x = alpha * vals[e];
+    kv[e] = x;
+    if (ut) {
+        const T c = fabs(alpha * vals[0]);
+        if (e == 0) {
+            ut->c = c;
+            if (!(c > (T)0) || !isfinite(c)) atomicOr(&ut->mixed, 1u);
+        }
+        if (in && fabs(x) != c) atomicOr(&ut->mixed, 1u);
+    }
 }
 
-// vrp[v] = first sorted position whose virtual row is >= v (invalid keys sort last); kl = k % SP_KC.
-__global__ void rowptr_kernel(int64_t nnz, const uint64_t *keys, int64_t NV, int32_t *vrp, uint16_t *kl) {
+// vrp[v] = first sorted position whose virtual row is >= v (invalid keys sort last); kl = k % SP_KC;
+// rec = byte offset of k % SP_KC in a panel column, sign of the value in bit 15 (the uniform-value
+// apply's entry record, section 4).
+template <typename T>
+__global__ void rowptr_kernel(int64_t nnz, const uint64_t *keys, const T *kv, int64_t NV, int32_t *vrp, uint16_t *kl,
+                              uint16_t *rec) {
     const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (e > nnz) return;
     const uint64_t inval = ~(uint64_t)0;
     const int64_t cur = (e < nnz && keys[e] != inval) ? (int64_t)(keys[e] / SP_KC) : NV;
     const int64_t prev = (e == 0) ? -1 : ((keys[e - 1] != inval) ? (int64_t)(keys[e - 1] / SP_KC) : NV);
     for (int64_t v = prev + 1; v <= cur && v <= NV; ++v) vrp[v] = (int32_t)e;
-    if (e < nnz && keys[e] != inval) kl[e] = (uint16_t)(keys[e] % SP_KC);
+    if (e < nnz && keys[e] != inval) {
+        const uint16_t k = (uint16_t)(keys[e] % SP_KC);
+        kl[e] = k;
+        rec[e] = (uint16_t)((k * sizeof(T)) | (signbit(kv[e]) ? 0x8000u : 0u));
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -333,7 +355,9 @@ __device__ __forceinline__ void sa_compute(T (&acc)[SA_R], const char *pcol, con
 template <typename T, bool VP>
 __global__ __launch_bounds__(SA_NT) __attribute__((amdgpu_waves_per_eu(SA_WPE_DEF))) void saso_apply_kernel(const SparseApply p, const int32_t *vrp,
                                                                        const uint16_t *kl, const T *kv,
-                                                                       int64_t nchunks, int64_t nrb) {
+                                                                       int64_t nchunks, int64_t nrb,
+                                                                       const uint32_t *mixed) {
+    if (mixed && *mixed == 0u) return;   // the uniform-value kernel (section 4) took this call
     // one LDS array, carved (panel | records | row pointers)
     constexpr int PANEL = SA_J * SA_LDP;
     constexpr int NREC = SA_EMAX + 1;
@@ -410,6 +434,316 @@ __global__ __launch_bounds__(SA_NT) __attribute__((amdgpu_waves_per_eu(SA_WPE_DE
         if (r < rem) cb[r * p.crs] = acc[r];
 }
 
+// ------------------------------------------------------------------------------------------
+// 4. Apply for uniform-magnitude operators: every in-window value is +c or -c (all sampled SASO /
+//    LASO operators, c = |alpha|). Then (alpha*v)*y = sign(v) * (c*y) exactly (round-to-nearest is
+//    sign-symmetric), so the panel is stored prescaled, P = c*Y, and an entry reduces to a 16-bit
+//    record (byte offset of k % SP_KC in a panel column, sign in bit 15):
+//    acc += sign ? -P(k, j) : P(k, j). Same order, same roundings as the reference's scalar loop.
+//
+//    Workgroup = 16 waves = 512 output rows x 64 output columns (lane = column); a wave owns 32
+//    consecutive rows with one accumulator per row per lane. Per chunk of SP_KC contracted
+//    indices:
+//      * the prescaled panel sits in LDS as [64 columns][SP_KC + 1] (the odd stride makes both the
+//        transposing stores and the lane-per-column reads conflict-free); element SP_KC of every
+//        column is zero, the "absent entry" slot. Two buffers: chunk c+1 is loaded into registers
+//        (coalesced, 16 B per lane along k) while chunk c is consumed, and stored behind it.
+//      * a slot table built with the CSR gives every (chunk, row) its first two entry records in
+//        one u32 (absent ones point at the zero slot with the sign bit set, adding -0.0, which
+//        leaves every accumulator bit-identical; bit 30 flags a third entry). Lane l of a wave
+//        holds the word of its row l, one chunk ahead, so the walk is: per row, one readlane,
+//        two LDS reads, two adds -- straight-line code over the 32 rows, 4 rows' reads in flight
+//        ahead of their adds. Rows with three or more entries in the chunk (about 8 % at C3)
+//        then walk the rest of their CSR range, in order.
+// ------------------------------------------------------------------------------------------
+constexpr int SU_NT = 1024;                   // threads per workgroup (16 waves)
+constexpr int SU_R = 32;                      // output rows per wave
+constexpr int SU_ROWS = SU_NT / 64 * SU_R;    // output rows per workgroup
+constexpr int SU_J = 64;                      // output columns per workgroup (lane = column)
+constexpr int SU_LDP = SP_KC + 1;             // panel column stride (elements)
+#ifndef SU_ABL
+#define SU_ABL 0   // diagnostics only: 1 skips the two-slot walk, 2 the third+ entries, 4 the panel loads
+#endif
+#ifndef SU_G_DEF
+#define SU_G_DEF 2
+#endif
+constexpr int SU_G = SU_G_DEF;                // rows whose slot reads are issued together (f64; f32 2x)
+constexpr uint32_t SU_NEG = 0x8000u;          // record sign bit
+constexpr uint32_t SU_MORE = 0x40000000u;     // slot word, high half: the row has a fifth entry
+template <typename T> __host__ __device__ constexpr uint32_t su_absent() {
+    return SU_NEG | (uint32_t)(SP_KC * sizeof(T));
+}
+
+template <typename T> __device__ __forceinline__ T su_flip(T y, uint32_t signbit31);
+template <> __device__ __forceinline__ double su_flip<double>(double y, uint32_t signbit31) {
+    return __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, y) ^ ((uint64_t)(signbit31 & 0x80000000u) << 32));
+}
+template <> __device__ __forceinline__ float su_flip<float>(float y, uint32_t signbit31) {
+    return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, y) ^ (signbit31 & 0x80000000u));
+}
+
+// slot[v] = records of the first four entries of virtual row v = chunk*M + row, 16 bits each
+// (absent ones: the zero slot, negative); SU_MORE in the fourth marks a fifth entry
+__global__ void slot_kernel(int64_t NV, const int32_t *vrp, const uint16_t *rec, uint32_t absent, uint64_t *slot) {
+    const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (v >= NV) return;
+    const int32_t a = vrp[v], n = vrp[v + 1] - a;
+    uint64_t w = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w |= (uint64_t)(n > q ? rec[a + q] : absent) << (16 * q);
+    if (n > 4) w |= (uint64_t)SU_MORE << 32;
+    slot[v] = w;
+}
+
+template <typename T> struct SuCfg {
+    static constexpr int VEC = 16 / (int)sizeof(T);                      // elements per 16-B vector
+    static constexpr int PANEL = SU_LDP * SU_J;                          // elements per buffer
+    static constexpr int LDR = SU_R + VEC;                               // epilogue: column stride
+    static constexpr int EPI = 8 * SU_J * LDR;                           // epilogue: 8 waves at a time
+    static constexpr int LDS_ELEMS = 2 * PANEL > EPI ? 2 * PANEL : EPI;
+    static constexpr int NST = SP_KC * SU_J / SU_NT;                     // panel elements per thread
+};
+
+// Panel staging. YJ (Y(k, j) contiguous along j): element e = tid + SU_NT*q is (k = e / 64,
+// column e % 64), one coalesced 512-B row per wave. Otherwise (contiguous along k, 16-B aligned,
+// K % VEC == 0): vector v = tid + SU_NT*q is (column v / (SP_KC/VEC), k = VEC * (v % (SP_KC/VEC))),
+// a wave reads 1 KB of one column. Out-of-range elements read a clamped address and are zeroed.
+template <typename T, bool YJ>
+__device__ __forceinline__ void su_panel_load(T (&st)[SuCfg<T>::NST], const SparseApply &p, int64_t c, int64_t j0,
+                                              int tid) {
+    typedef SuCfg<T> G;
+    const T *Y = (const T *)p.Y;
+    const int64_t kc0 = c * SP_KC;
+    if (YJ) {
+#pragma unroll
+        for (int q = 0; q < G::NST; ++q) {
+            const int e = tid + SU_NT * q;
+            const int64_t gk = kc0 + e / SU_J, gj = j0 + e % SU_J;
+            const bool ok = gk < p.K && gj < p.N;
+            const T x = Y[(ok ? gk : 0) * p.ysk + (ok ? gj : 0)];
+            st[q] = ok ? x : (T)0;
+        }
+    } else {
+        constexpr int VEC = G::VEC;
+        typedef T v_t __attribute__((ext_vector_type(VEC)));
+#pragma unroll
+        for (int q = 0; q < G::NST / VEC; ++q) {
+            const int v = tid + SU_NT * q;
+            const int64_t gj = j0 + v / (SP_KC / VEC), gk = kc0 + VEC * (v % (SP_KC / VEC));
+            const bool ok = gk < p.K && gj < p.N;
+            const v_t x = *reinterpret_cast<const v_t *>(Y + (ok ? gj * p.ysj + gk : 0));
+#pragma unroll
+            for (int t = 0; t < VEC; ++t) st[q * VEC + t] = ok ? x[t] : (T)0;
+        }
+    }
+}
+
+template <typename T, bool YJ>
+__device__ __forceinline__ void su_panel_store(const T (&st)[SuCfg<T>::NST], T *buf, T c, int tid) {
+    typedef SuCfg<T> G;
+    if (YJ) {
+#pragma unroll
+        for (int q = 0; q < G::NST; ++q) {
+            const int e = tid + SU_NT * q;
+            buf[(e % SU_J) * SU_LDP + e / SU_J] = c * st[q];
+        }
+    } else {
+        constexpr int VEC = G::VEC;
+#pragma unroll
+        for (int q = 0; q < G::NST / VEC; ++q) {
+            const int v = tid + SU_NT * q;
+            T *d = buf + (v / (SP_KC / VEC)) * SU_LDP + VEC * (v % (SP_KC / VEC));
+#pragma unroll
+            for (int t = 0; t < VEC; ++t) d[t] = c * st[q * VEC + t];
+        }
+    }
+}
+
+// the signed prescaled panel value of a record for this lane's column (lanex = column base, bytes)
+template <typename T>
+__device__ __forceinline__ T su_read(const char *lds, uint32_t lanex, uint32_t off) {
+    return *reinterpret_cast<const T *>(lds + lanex + off);
+}
+
+template <typename T, bool YJ>
+__global__ __launch_bounds__(SU_NT) void saso_unit_kernel(const SparseApply p, const int32_t *vrp,
+                                                          const uint16_t *rec16, const uint64_t *slot,
+                                                          int64_t nchunks, int64_t nrb, const UniformTest<T> *ut,
+                                                          int vec_out) {
+    if (ut->mixed) return;   // values of more than one magnitude: saso_apply_kernel takes the call
+    typedef SuCfg<T> G;
+    __shared__ __attribute__((aligned(16))) T lds[G::LDS_ELEMS];
+    const char *lbase = reinterpret_cast<const char *>(lds);
+    const T c = ut->c;
+
+    const int tid = threadIdx.x;
+    const uint32_t lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t nb = (int64_t)gridDim.x;
+    const int64_t b = blockIdx.x;
+    const int64_t xcd = b % 8, qq = nb / 8, rr = nb % 8;
+    const int64_t t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + b / 8;
+    const int64_t rb0 = (t % nrb) * SU_ROWS;
+    const int64_t j0 = (t / nrb) * SU_J;
+    const int64_t row0 = rb0 + (int64_t)wave * SU_R;
+    const int64_t j = j0 + lane;
+    const bool jin = j < p.N;
+    T *C = (T *)p.C;
+    const T beta = (T)p.beta;
+
+    // zero slots of both buffers
+    if (tid < 2 * SU_J) lds[(tid / SU_J) * G::PANEL + (tid % SU_J) * SU_LDP + SP_KC] = (T)0;
+
+    T acc[SU_R];
+    if (beta != (T)0) {
+        int64_t off = row0 * p.crs + j * p.ccs;
+        asm volatile("" : "+v"(off));
+        const T *cb = C + off;
+#pragma unroll
+        for (int r = 0; r < SU_R; ++r) acc[r] = (jin && row0 + r < p.M) ? beta * cb[r * p.crs] : (T)0;
+    } else {
+#pragma unroll
+        for (int r = 0; r < SU_R; ++r) acc[r] = (T)0;
+    }
+
+    // slot words of chunk cc: lane l < SU_R holds row row0 + l (rows past M: all slots absent);
+    // .x = first two records, .y = third and fourth
+    constexpr uint32_t ABS2 = su_absent<T>() | (su_absent<T>() << 16);
+    auto load_slot = [&](int64_t cc) -> uint2 {
+        const int64_t r = row0 + (int64_t)(lane & (SU_R - 1));
+        const bool ok = r < p.M && lane < (uint32_t)SU_R;
+        const uint64_t w = slot[cc * p.M + (ok ? r : 0)];
+        return ok ? make_uint2((uint32_t)w, (uint32_t)(w >> 32)) : make_uint2(ABS2, ABS2);
+    };
+
+    T st[G::NST];
+    const uint32_t lane0 = lane * (uint32_t)(SU_LDP * sizeof(T));
+    uint2 sl_c = load_slot(0);
+    if (!(SU_ABL & 4)) su_panel_load<T, YJ>(st, p, 0, j0, tid);
+    su_panel_store<T, YJ>(st, lds, c, tid);
+    __syncthreads();
+
+    for (int64_t ch = 0; ch < nchunks; ++ch) {
+        const bool more = ch + 1 < nchunks;
+        uint2 sl_n = make_uint2(0u, 0u);
+        if (more) {
+            sl_n = load_slot(ch + 1);
+            if (!(SU_ABL & 4)) su_panel_load<T, YJ>(st, p, ch + 1, j0, tid);
+        }
+        const uint32_t lanex = lane0 + (uint32_t)((ch & 1) * G::PANEL * sizeof(T));
+        if (!(SU_ABL & 1)) {
+            // rows' first two entries, SU_G rows at a time, software-pipelined: the reads of group
+            // g + 1 are issued before the adds of group g (sched_barrier keeps the compiler from
+            // hoisting every group's reads, which would need two registers per row)
+            constexpr int GG = sizeof(T) == 8 ? SU_G : 2 * SU_G;
+            auto reads = [&](int r, T &y0, T &y1, uint32_t &w) {
+                w = (uint32_t)__builtin_amdgcn_readlane((int)sl_c.x, r);
+                y0 = su_read<T>(lbase, lanex, w & 0x3fffu);
+                y1 = su_read<T>(lbase, lanex, (w >> 16) & 0x3fffu);
+            };
+            T ya[GG][2], yb[GG][2];
+            uint32_t wa[GG], wb[GG];
+#pragma unroll
+            for (int q = 0; q < GG; ++q) reads(q, ya[q][0], ya[q][1], wa[q]);
+#pragma unroll
+            for (int g = 0; g < SU_R; g += GG) {
+                const bool odd = (g / GG) & 1;
+                T (&cy)[GG][2] = odd ? yb : ya;
+                T (&ny)[GG][2] = odd ? ya : yb;
+                uint32_t (&cw)[GG] = odd ? wb : wa;
+                uint32_t (&nw)[GG] = odd ? wa : wb;
+                if (g + GG < SU_R) {
+#pragma unroll
+                    for (int q = 0; q < GG; ++q) reads(g + GG + q, ny[q][0], ny[q][1], nw[q]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int q = 0; q < GG; ++q) {
+                    T s = acc[g + q] + su_flip<T>(cy[q][0], cw[q] << 16);
+                    s = s + su_flip<T>(cy[q][1], cw[q]);
+                    acc[g + q] = s;
+                    asm volatile("" : "+v"(acc[g + q]));   // the adds stay here, not sunk below
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if (!(SU_ABL & 2)) {
+            // rows with a third entry (about 8 % at C3): entries 3 and 4 from the slot word, in
+            // order; a fifth and later (0.4 %) from the CSR in memory
+            const uint64_t more3 = __builtin_amdgcn_ballot_w64((sl_c.y & 0xffffu) != su_absent<T>());
+            if (more3) {
+#pragma unroll
+                for (int r = 0; r < SU_R; ++r) {
+                    if ((more3 >> r) & 1u) {
+                        const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)sl_c.y, r);
+                        const T y2 = su_read<T>(lbase, lanex, w & 0x3fffu);
+                        const T y3 = su_read<T>(lbase, lanex, (w >> 16) & 0x3fffu);
+                        T s = acc[r] + su_flip<T>(y2, w << 16);
+                        s = s + su_flip<T>(y3, w);
+                        if (w & SU_MORE) {
+                            const int64_t v = ch * p.M + row0 + r;
+                            const int a = vrp[v], e = vrp[v + 1];
+#pragma unroll 1
+                            for (int x = a + 4; x < e; ++x) {
+                                const uint32_t q = rec16[x];
+                                s = s + su_flip<T>(su_read<T>(lbase, lanex, q & 0x3fffu), q << 16);
+                            }
+                        }
+                        acc[r] = s;
+                    }
+                }
+            }
+        }
+        if (more) su_panel_store<T, YJ>(st, lds + ((ch + 1) & 1) * G::PANEL, c, tid);
+        __syncthreads();
+        sl_c = sl_n;
+    }
+
+    // epilogue
+    if (vec_out) {
+        // C column-contiguous (crs == 1), 16-B aligned columns: stage each wave's 32 x 64 block in
+        // LDS (column stride LDR) and store 16-B vectors along the columns, 8 waves per round
+        constexpr int VEC = G::VEC;
+        typedef T v_t __attribute__((ext_vector_type(VEC)));
+#pragma unroll
+        for (int round = 0; round < 2; ++round) {
+            const bool mine = (wave >> 3) == round;
+            T *reg = lds + (wave & 7) * SU_J * G::LDR;
+            if (mine) {
+#pragma unroll
+                for (int r = 0; r < SU_R; ++r) reg[lane * G::LDR + r] = acc[r];
+            }
+            __syncthreads();
+            if (mine) {
+                constexpr int VPC = SU_R / VEC;   // vectors per column
+#pragma unroll
+                for (int q = 0; q < SU_J * VPC / 64; ++q) {
+                    const int v = lane + 64 * q;
+                    const int col = v / VPC, rv = (v % VPC) * VEC;
+                    const int64_t gi = row0 + rv, gj = j0 + col;
+                    if (gj < p.N) {
+                        const v_t x = *reinterpret_cast<const v_t *>(reg + col * G::LDR + rv);
+                        T *dst = C + gi + gj * p.ccs;
+                        if (gi + VEC <= p.M) *reinterpret_cast<v_t *>(dst) = x;
+                        else
+                            for (int u = 0; u < VEC; ++u)
+                                if (gi + u < p.M) dst[u] = x[u];
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    } else if (jin) {
+        // output base behind an opaque move, so per-row addresses are not kept live across the walk
+        int64_t off = row0 * p.crs + j * p.ccs;
+        asm volatile("" : "+v"(off));
+        T *cb = C + off;
+#pragma unroll
+        for (int r = 0; r < SU_R; ++r)
+            if (row0 + r < p.M) cb[r * p.crs] = acc[r];
+    }
+}
+
 template <typename T>
 static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, const int64_t *cols, const T *vals,
                                      int64_t nnz, hipStream_t s) {
@@ -433,7 +767,8 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
     err = rocprim::radix_sort_pairs(nullptr, tmp_bytes, k_in, k_out, v_in, v_out, n, 0, (unsigned)end_bit, s);
     if (err != hipSuccess) return err;
     const size_t bytes = 2 * n * sizeof(uint64_t) + 2 * n * sizeof(T) + (size_t)(NV + 1) * sizeof(int32_t) +
-                         n * sizeof(uint16_t) + tmp_bytes + 256;
+                         2 * n * sizeof(uint16_t) + (size_t)(NV > 0 ? NV : 1) * sizeof(uint64_t) + sizeof(UniformTest<T>) +
+                         tmp_bytes + 512;
     char *ws = nullptr;
     err = hipMallocAsync((void **)&ws, bytes, s);
     if (err != hipSuccess) return err;
@@ -445,24 +780,50 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
     v_out = (T *)carve(n * sizeof(T));
     vrp = (int32_t *)carve((size_t)(NV + 1) * sizeof(int32_t));
     kl = (uint16_t *)carve(n * sizeof(uint16_t));
+    uint16_t *rec = (uint16_t *)carve(n * sizeof(uint16_t));
+    uint64_t *slot = (uint64_t *)carve((size_t)(NV > 0 ? NV : 1) * sizeof(uint64_t));
+    UniformTest<T> *ut = (UniformTest<T> *)carve(sizeof(UniformTest<T>));
     tmp = carve(tmp_bytes);
+
+    // The uniform-value kernel needs Y contiguous along j, or along k in 16-B vectors.
+    constexpr int VEC = SuCfg<T>::VEC;
+    const bool y_j = p.ysj == 1;
+    const bool y_k = p.ysk == 1 && (p.ysj % VEC) == 0 && (((uintptr_t)p.Y) % 16) == 0 && (p.K % VEC) == 0;
+    static const bool unit_off = [] { const char *e = getenv("RBH_NO_SASO_UNIT"); return e && e[0] == '1'; }();
+    const bool unit = (y_j || y_k) && !unit_off;
+    err = hipMemsetAsync(ut, 0, sizeof(UniformTest<T>), s);
+    if (err != hipSuccess) { (void)hipFreeAsync(ws, s); return err; }
 
     if (nnz > 0) {
         hipLaunchKernelGGL(coo_keys_kernel<T>, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, rows, cols,
-                           vals, p.ro, p.co, p.win_r, p.win_c, p.transposed, p.M, (T)p.alpha, k_in, v_in);
+                           vals, p.ro, p.co, p.win_r, p.win_c, p.transposed, p.M, (T)p.alpha, k_in, v_in,
+                           unit ? ut : nullptr);
         // invalid keys (~0) still sort last: their low end_bit bits are all ones, above every valid key
         err = rocprim::radix_sort_pairs(tmp, tmp_bytes, k_in, k_out, v_in, v_out, (size_t)nnz, 0, (unsigned)end_bit, s);
         if (err != hipSuccess) { (void)hipFreeAsync(ws, s); return err; }
     }
-    hipLaunchKernelGGL(rowptr_kernel, dim3((unsigned)((nnz + 1 + 255) / 256)), dim3(256), 0, s, nnz, k_out, NV, vrp,
-                       kl);
+    hipLaunchKernelGGL(rowptr_kernel<T>, dim3((unsigned)((nnz + 1 + 255) / 256)), dim3(256), 0, s, nnz, k_out, v_out,
+                       NV, vrp, kl, rec);
+    if (unit && NV > 0)
+        hipLaunchKernelGGL(slot_kernel, dim3((unsigned)((NV + 255) / 256)), dim3(256), 0, s, NV, vrp, rec,
+                           su_absent<T>(), slot);
+    timing_begin(s);
+    if (unit) {
+        const int64_t nrb_u = (p.M + SU_ROWS - 1) / SU_ROWS;
+        const dim3 grid_u((unsigned)(((p.N + SU_J - 1) / SU_J) * nrb_u));
+        const int vec_out = p.crs == 1 && (p.ccs % VEC) == 0 && (((uintptr_t)p.C) % 16) == 0;
+        if (y_j) hipLaunchKernelGGL((saso_unit_kernel<T, true>), grid_u, dim3(SU_NT), 0, s, p, vrp, rec, slot, nchunks, nrb_u, ut, vec_out);
+        else hipLaunchKernelGGL((saso_unit_kernel<T, false>), grid_u, dim3(SU_NT), 0, s, p, vrp, rec, slot, nchunks, nrb_u, ut, vec_out);
+    }
+    // general values (or a layout the kernel above does not take): exits at once when the
+    // uniform-value kernel ran
     const int64_t nrb = (p.M + SA_ROWS - 1) / SA_ROWS;
     const dim3 grid((unsigned)(((p.N + SA_J - 1) / SA_J) * nrb));
-    timing_begin(s);
+    const uint32_t *mixed = unit ? &ut->mixed : nullptr;
     const bool vecpanel = p.ysk == 1 && (p.ysj % PanelVec<T>::N) == 0 && (((uintptr_t)p.Y) % 16) == 0 &&
                           (p.K % PanelVec<T>::N) == 0;
-    if (vecpanel) hipLaunchKernelGGL((saso_apply_kernel<T, true>), grid, dim3(SA_NT), 0, s, p, vrp, kl, v_out, nchunks, nrb);
-    else hipLaunchKernelGGL((saso_apply_kernel<T, false>), grid, dim3(SA_NT), 0, s, p, vrp, kl, v_out, nchunks, nrb);
+    if (vecpanel) hipLaunchKernelGGL((saso_apply_kernel<T, true>), grid, dim3(SA_NT), 0, s, p, vrp, kl, v_out, nchunks, nrb, mixed);
+    else hipLaunchKernelGGL((saso_apply_kernel<T, false>), grid, dim3(SA_NT), 0, s, p, vrp, kl, v_out, nchunks, nrb, mixed);
     err = hipGetLastError();
     timing_end(s);
     hipError_t e2 = hipFreeAsync(ws, s);

@@ -52,13 +52,16 @@ def test_fill_sparse_bitwise(cuda, dims, vec_nnz, major, key):
     assert np.array_equal(host(dv), vals)
 
 
-def check_left(cuda, layout, opS, opA, d, n, m, alpha, beta, SR, SC, vec, major, key, ro, co, dtype, given=False):
+def check_left(cuda, layout, opS, opA, d, n, m, alpha, beta, SR, SC, vec, major, key, ro, co, dtype, given=False,
+               vals_fn=None):
     rA, cA = (m, n) if opA == "N" else (n, m)
     A = O.random_matrix(rA, cA, 99, dtype)
     lda = rA if layout == "C" else cA
     B0 = O.random_matrix(d, n, 42, dtype)
     ldb = d if layout == "C" else n
     rows, cols, vals = O.fill_sparse(SR, SC, vec, major, key=key, dtype=dtype)
+    if vals_fn is not None:   # user values instead of the sampled +-1
+        vals = vals_fn(vals).astype(dtype)
     Bexp = B0.copy()
     O.left_spmm_coo(layout, opS, opA, d, n, m, alpha, SR, SC, rows, cols, vals, ro, co, A, lda, beta, Bexp, ldb)
     S = rb.SparseSkOp(rb.SparseDist(SR, SC, vec, major), rb.RNGState(key=key))
@@ -98,6 +101,33 @@ def test_lskges_submatrix_ops(cuda, major, opS, opA, layout, dtype):
 def test_lskges_user_coo(cuda, layout):
     check_left(cuda, layout, "N", "N", 19, 12, 201, 0.5, -1.0, 19, 201, 7, "S", 0, 0, 0, np.float64, given=True)
     check_left(cuda, layout, "T", "N", 19, 12, 201, 0.5, 0.0, 201, 19, 7, "S", 0, 0, 0, np.float64, given=True)
+
+
+@pytest.mark.parametrize("layout", ["C", "R"])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_lskges_user_values(cuda, layout, dtype):
+    """User COO arrays whose values are not all of one magnitude take the general-value kernel;
+    +-c arrays (c != 1) and arrays with a single odd value exercise the magnitude test."""
+    rng = np.random.default_rng(3)
+    general = lambda v: rng.standard_normal(v.shape)
+    scaled = lambda v: 2.5 * v
+    one_odd = lambda v: np.where(np.arange(v.size) == v.size // 2, 3.0 * v, v)
+    for fn in (general, scaled, one_odd):
+        check_left(cuda, layout, "N", "N", 19, 12, 201, 0.5, -1.0, 19, 201, 7, "S", 0, 0, 0, dtype, given=True,
+                   vals_fn=fn)
+        check_left(cuda, layout, "N", "N", 300, 70, 1000, 1.0, 0.0, 300, 1000, 4, "S", 1, 0, 0, dtype, given=True,
+                   vals_fn=fn)
+
+
+@pytest.mark.parametrize("layout", ["C", "R"])
+@pytest.mark.parametrize("opA", ["N", "T"])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("d,n,m,vec", [(1000, 130, 2048, 8),    # two 512-row blocks, ragged rows and columns
+                                       (64, 70, 1024, 8),       # ~16 entries per row per chunk: >64 per wave
+                                       (520, 65, 640, 1)])      # sparse rows: most first slots absent
+def test_lskges_apply_shapes(cuda, layout, opA, dtype, d, n, m, vec):
+    check_left(cuda, layout, "N", opA, d, n, m, 1.0, 0.0, d, m, vec, "S", 7, 0, 0, dtype)
+    check_left(cuda, layout, "N", opA, d, n, m, -2.0, 0.5, d, m, vec, "S", 8, 0, 0, dtype)
 
 
 def test_lskges_config3_slice(cuda):
