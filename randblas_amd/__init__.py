@@ -347,6 +347,20 @@ def sketch_general(layout, op1, op2, d_or_m, n_or_d, m_or_n, alpha, X, Y, lda_or
     return sketch_general_right(layout, op1, op2, d_or_m, n_or_d, m_or_n, alpha, X, Y, lda_or_none, *args, **kw)
 
 
+def sketch_vector(opS, d, m, alpha, S, x, incx, beta, y, incy, ro_s=0, co_s=0, stream=None):
+    """y = alpha op(submat(S)) x + beta y, with submat(S) of size d x m (RandBLAS/skve.hh:152-176).
+
+    As in the reference this is sketch_general in RowMajor with n = 1, lda = incx and ldb = incy;
+    (d, m) are the dimensions of submat(S) before op, so they swap roles for opS = "T"."""
+    _d, _m = (d, m) if opS == "N" else (m, d)
+    sketch_general_left("R", opS, "N", _d, 1, _m, alpha, S, x, incx, beta, y, incy, ro_s, co_s, stream)
+
+
+def sketch_vector_full(opS, alpha, S, x, incx, beta, y, incy, stream=None):
+    """y = alpha op(S) x + beta y over the whole operator (RandBLAS/skve.hh:244-258)."""
+    sketch_vector(opS, S.dist.n_rows, S.dist.n_cols, alpha, S, x, incx, beta, y, incy, 0, 0, stream)
+
+
 def kernel_timing(on: bool) -> None:
     """Enable/disable HIP-event timing of each call's dominant kernel (diagnostics)."""
     lib.rbh_kernel_timing_enable(1 if on else 0)
@@ -367,5 +381,5 @@ __all__ = [
     "RNGState", "DenseDist", "SparseDist", "DenseSkOp", "SparseSkOp", "RandBLASError", "fill_dense", "fill_sparse",
     "sketch_general", "sketch_general_left", "sketch_general_right", "sketch_symmetric_left",
     "sketch_symmetric_right", "require_symmetric", "dense_next_state", "sparse_next_state", "abi_version", "lib",
-    "LIB_PATH", "kernel_timing", "kernel_times_ms",
+    "LIB_PATH", "kernel_timing", "kernel_times_ms", "sketch_vector", "sketch_vector_full",
 ]

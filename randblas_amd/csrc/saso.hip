@@ -140,11 +140,11 @@ __global__ void coo_keys_kernel(int64_t nnz, const int64_t *rows, const int64_t 
 }
 
 // vrp[v] = first sorted position whose virtual row is >= v (invalid keys sort last); kl = k % SP_KC;
-// rec = byte offset of k % SP_KC in a panel column, sign of the value in bit 15 (the uniform-value
-// apply's entry record, section 4).
+// rec = the uniform-value apply's entry record (section 4): panel byte offset of k % SP_KC, the
+// accumulator register index of the row within its wave, sign of the value.
 template <typename T>
-__global__ void rowptr_kernel(int64_t nnz, const uint64_t *keys, const T *kv, int64_t NV, int32_t *vrp, uint16_t *kl,
-                              uint16_t *rec) {
+__global__ void rowptr_kernel(int64_t nnz, const uint64_t *keys, const T *kv, int64_t NV, int64_t M, int32_t *vrp,
+                              uint16_t *kl, uint32_t *rec) {
     const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (e > nnz) return;
     const uint64_t inval = ~(uint64_t)0;
@@ -154,7 +154,9 @@ __global__ void rowptr_kernel(int64_t nnz, const uint64_t *keys, const T *kv, in
     if (e < nnz && keys[e] != inval) {
         const uint16_t k = (uint16_t)(keys[e] % SP_KC);
         kl[e] = k;
-        rec[e] = (uint16_t)((k * sizeof(T)) | (signbit(kv[e]) ? 0x8000u : 0u));
+        const uint32_t row = (uint32_t)((keys[e] / SP_KC) % (uint64_t)M) % 32u;   // row within its wave
+        rec[e] = (sizeof(T) == 8 ? 2u * row : row) | ((uint32_t)(k * sizeof(T)) << 8) |
+                 (signbit(kv[e]) ? 0x80000000u : 0u);
     }
 }
 
@@ -437,63 +439,43 @@ __global__ __launch_bounds__(SA_NT) __attribute__((amdgpu_waves_per_eu(SA_WPE_DE
 // ------------------------------------------------------------------------------------------
 // 4. Apply for uniform-magnitude operators: every in-window value is +c or -c (all sampled SASO /
 //    LASO operators, c = |alpha|). Then (alpha*v)*y = sign(v) * (c*y) exactly (round-to-nearest is
-//    sign-symmetric), so the panel is stored prescaled, P = c*Y, and an entry reduces to a 16-bit
-//    record (byte offset of k % SP_KC in a panel column, sign in bit 15):
-//    acc += sign ? -P(k, j) : P(k, j). Same order, same roundings as the reference's scalar loop.
+//    sign-symmetric), so the panel is stored prescaled, P = c*Y, and an entry becomes
+//    acc_i += (sign bit of v) ^ P(k, j), one add: the same single rounding of the same sum, in
+//    the same order, as the reference's scalar loop.
 //
 //    Workgroup = 16 waves = 512 output rows x 64 output columns (lane = column); a wave owns 32
 //    consecutive rows with one accumulator per row per lane. Per chunk of SP_KC contracted
 //    indices:
 //      * the prescaled panel sits in LDS as [64 columns][SP_KC + 1] (the odd stride makes both the
 //        transposing stores and the lane-per-column reads conflict-free); element SP_KC of every
-//        column is zero, the "absent entry" slot. Two buffers: chunk c+1 is loaded into registers
-//        (coalesced, 16 B per lane along k) while chunk c is consumed, and stored behind it.
-//      * a slot table built with the CSR gives every (chunk, row) its first two entry records in
-//        one u32 (absent ones point at the zero slot with the sign bit set, adding -0.0, which
-//        leaves every accumulator bit-identical; bit 30 flags a third entry). Lane l of a wave
-//        holds the word of its row l, one chunk ahead, so the walk is: per row, one readlane,
-//        two LDS reads, two adds -- straight-line code over the 32 rows, 4 rows' reads in flight
-//        ahead of their adds. Rows with three or more entries in the chunk (about 8 % at C3)
-//        then walk the rest of their CSR range, in order.
+//        column is zero. Two buffers: chunk c+1 is loaded into registers (coalesced, 16 B per
+//        lane along k) while chunk c is consumed, and stored behind it.
+//      * the wave's entries of the chunk -- its 32 rows, each in ascending k, about 32 at C3 -- are
+//        one contiguous CSR range. Lane e holds record e (32 bits: panel byte offset, the row's
+//        accumulator register index, sign), loaded one chunk ahead. The walk is flat over the
+//        range, four entries per step with their LDS reads issued a step ahead; each entry is
+//        one readlane, a few scalar ops, one LDS read, a sign xor and one v_add whose accumulator
+//        operand is selected by the row through GPR index mode (s_set_gpr_idx_on), so a row's position in
+//        the range costs nothing and no row reads an entry it does not have. Padding entries
+//        read the zero element with sign -1 and add -0.0, which leaves an accumulator
+//        bit-identical.
 // ------------------------------------------------------------------------------------------
 constexpr int SU_NT = 1024;                   // threads per workgroup (16 waves)
 constexpr int SU_R = 32;                      // output rows per wave
 constexpr int SU_ROWS = SU_NT / 64 * SU_R;    // output rows per workgroup
 constexpr int SU_J = 64;                      // output columns per workgroup (lane = column)
 constexpr int SU_LDP = SP_KC + 1;             // panel column stride (elements)
+#ifndef SU_D_DEF
+#define SU_D_DEF 4
+#endif
+constexpr int SU_D = SU_D_DEF;                // entries per walk step
+constexpr int SU_WIN = 64 - 2 * SU_D;         // records per register window
 #ifndef SU_ABL
-#define SU_ABL 0   // diagnostics only: 1 skips the two-slot walk, 2 the third+ entries, 4 the panel loads
+#define SU_ABL 0   // diagnostics only: 1 skips the walk, 4 the panel loads, 8 static-row updates, 16 no walk reads
 #endif
-#ifndef SU_G_DEF
-#define SU_G_DEF 2
-#endif
-constexpr int SU_G = SU_G_DEF;                // rows whose slot reads are issued together (f64; f32 2x)
-constexpr uint32_t SU_NEG = 0x8000u;          // record sign bit
-constexpr uint32_t SU_MORE = 0x40000000u;     // slot word, high half: the row has a fifth entry
-template <typename T> __host__ __device__ constexpr uint32_t su_absent() {
-    return SU_NEG | (uint32_t)(SP_KC * sizeof(T));
-}
-
-template <typename T> __device__ __forceinline__ T su_flip(T y, uint32_t signbit31);
-template <> __device__ __forceinline__ double su_flip<double>(double y, uint32_t signbit31) {
-    return __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, y) ^ ((uint64_t)(signbit31 & 0x80000000u) << 32));
-}
-template <> __device__ __forceinline__ float su_flip<float>(float y, uint32_t signbit31) {
-    return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, y) ^ (signbit31 & 0x80000000u));
-}
-
-// slot[v] = records of the first four entries of virtual row v = chunk*M + row, 16 bits each
-// (absent ones: the zero slot, negative); SU_MORE in the fourth marks a fifth entry
-__global__ void slot_kernel(int64_t NV, const int32_t *vrp, const uint16_t *rec, uint32_t absent, uint64_t *slot) {
-    const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (v >= NV) return;
-    const int32_t a = vrp[v], n = vrp[v + 1] - a;
-    uint64_t w = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) w |= (uint64_t)(n > q ? rec[a + q] : absent) << (16 * q);
-    if (n > 4) w |= (uint64_t)SU_MORE << 32;
-    slot[v] = w;
-}
+// record: bits 0-5 accumulator register index (2 x row for f64, row for f32; s_set_gpr_idx_on reads
+// bits 0-7), bits 8-18 panel byte offset of k % SP_KC, bit 31 the sign of the value
+template <typename T> __host__ __device__ constexpr uint32_t su_pad() { return 0x80000000u | ((uint32_t)(SP_KC * sizeof(T)) << 8); }
 
 template <typename T> struct SuCfg {
     static constexpr int VEC = 16 / (int)sizeof(T);                      // elements per 16-B vector
@@ -559,17 +541,53 @@ __device__ __forceinline__ void su_panel_store(const T (&st)[SuCfg<T>::NST], T *
     }
 }
 
-// the signed prescaled panel value of a record for this lane's column (lanex = column base, bytes)
-template <typename T>
-__device__ __forceinline__ T su_read(const char *lds, uint32_t lanex, uint32_t off) {
-    return *reinterpret_cast<const T *>(lds + lanex + off);
-}
+// The accumulators: 32 rows per lane in two pinned register blocks, v[32:63] and v[64:95] for f64
+// (v[32:63] for f32), so that GPR index mode can address row i's accumulator as v32 + idx.
+template <typename T> struct SuAcc;
+template <> struct SuAcc<double> {
+    typedef double v16 __attribute__((ext_vector_type(16)));
+    v16 a, b;   // rows 0-15, 16-31
+    __device__ __forceinline__ double get(int r) const { return r < 16 ? a[r] : b[r - 16]; }
+    __device__ __forceinline__ void set(int r, double x) { if (r < 16) a[r] = x; else b[r - 16] = x; }
+    // acc[row] += (sign bit of rec) ? -y : y, row's register index in rec bits 0-7 (the bits
+    // s_set_gpr_idx_on reads)
+    __device__ __forceinline__ void add_at(uint32_t rec, double y) {
+        const double ys = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, y) ^ ((uint64_t)(rec & 0x80000000u) << 32));
+        if (SU_ABL & 8) { a[0] += ys; return; }   // diagnostics: static row
+        asm volatile("s_set_gpr_idx_on %2, gpr_idx(SRC0,DST)\n\t"
+                     "v_add_f64 v[32:33], v[32:33], %3\n\t"
+                     "s_set_gpr_idx_off"
+                     : "+{v[32:63]}"(a), "+{v[64:95]}"(b)
+                     : "s"(rec), "v"(ys)
+                     : "m0");
+    }
+};
+template <> struct SuAcc<float> {
+    typedef float v32 __attribute__((ext_vector_type(32)));
+    v32 a;
+    __device__ __forceinline__ float get(int r) const { return a[r]; }
+    __device__ __forceinline__ void set(int r, float x) { a[r] = x; }
+    // The sign flip is inside the asm, from a scalar mask: when the compiler fused it into a
+    // v_bitop3_b32 reading the record's SGPR right before s_set_gpr_idx_on on that SGPR, whole
+    // entries were intermittently lost on gfx950 (tests/test_gpu_sparse.py user-values cases).
+    __device__ __forceinline__ void add_at(uint32_t rec, float y) {
+        if (SU_ABL & 8) { a[0] += __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, y) ^ (rec & 0x80000000u)); return; }
+        float t;
+        asm volatile("v_xor_b32 %1, %3, %4\n\t"
+                     "s_set_gpr_idx_on %2, gpr_idx(SRC0,DST)\n\t"
+                     "v_add_f32 v32, v32, %1\n\t"
+                     "s_set_gpr_idx_off"
+                     : "+{v[32:63]}"(a), "=&v"(t)
+                     : "s"(__builtin_amdgcn_readfirstlane(rec)), "s"(__builtin_amdgcn_readfirstlane(rec & 0x80000000u)),
+                       "v"(y)
+                     : "m0");
+    }
+};
 
 template <typename T, bool YJ>
 __global__ __launch_bounds__(SU_NT) void saso_unit_kernel(const SparseApply p, const int32_t *vrp,
-                                                          const uint16_t *rec16, const uint64_t *slot,
-                                                          int64_t nchunks, int64_t nrb, const UniformTest<T> *ut,
-                                                          int vec_out) {
+                                                          const uint32_t *rec32, int64_t nchunks, int64_t nrb,
+                                                          const UniformTest<T> *ut, int vec_out) {
     if (ut->mixed) return;   // values of more than one magnitude: saso_apply_kernel takes the call
     typedef SuCfg<T> G;
     __shared__ __attribute__((aligned(16))) T lds[G::LDS_ELEMS];
@@ -591,112 +609,101 @@ __global__ __launch_bounds__(SU_NT) void saso_unit_kernel(const SparseApply p, c
     T *C = (T *)p.C;
     const T beta = (T)p.beta;
 
-    // zero slots of both buffers
+    // zero elements of both buffers
     if (tid < 2 * SU_J) lds[(tid / SU_J) * G::PANEL + (tid % SU_J) * SU_LDP + SP_KC] = (T)0;
 
-    T acc[SU_R];
+    SuAcc<T> acc;
     if (beta != (T)0) {
         int64_t off = row0 * p.crs + j * p.ccs;
         asm volatile("" : "+v"(off));
         const T *cb = C + off;
 #pragma unroll
-        for (int r = 0; r < SU_R; ++r) acc[r] = (jin && row0 + r < p.M) ? beta * cb[r * p.crs] : (T)0;
+        for (int r = 0; r < SU_R; ++r) acc.set(r, (jin && row0 + r < p.M) ? beta * cb[r * p.crs] : (T)0);
     } else {
 #pragma unroll
-        for (int r = 0; r < SU_R; ++r) acc[r] = (T)0;
+        for (int r = 0; r < SU_R; ++r) acc.set(r, (T)0);
     }
 
-    // slot words of chunk cc: lane l < SU_R holds row row0 + l (rows past M: all slots absent);
-    // .x = first two records, .y = third and fourth
-    constexpr uint32_t ABS2 = su_absent<T>() | (su_absent<T>() << 16);
-    auto load_slot = [&](int64_t cc) -> uint2 {
-        const int64_t r = row0 + (int64_t)(lane & (SU_R - 1));
-        const bool ok = r < p.M && lane < (uint32_t)SU_R;
-        const uint64_t w = slot[cc * p.M + (ok ? r : 0)];
-        return ok ? make_uint2((uint32_t)w, (uint32_t)(w >> 32)) : make_uint2(ABS2, ABS2);
+    // entry range of chunk cc for this wave: lane 0 holds its start, lane 1 its end
+    const int64_t rlo = row0 < p.M ? row0 : p.M;
+    const int64_t rhi = row0 + SU_R < p.M ? row0 + SU_R : p.M;
+    auto load_bounds = [&](int64_t cc) -> int { return vrp[cc * p.M + (lane == 0 ? rlo : rhi)]; };
+    // record e of a range starting at eb in lane e < SU_WIN (past the range or window: padding)
+    auto load_recs = [&](int bnd) -> uint32_t {
+        const int eb = __builtin_amdgcn_readlane(bnd, 0), ee = __builtin_amdgcn_readlane(bnd, 1);
+        const int e0 = eb + (int)lane;
+        const bool in = e0 < ee && (int)lane < SU_WIN;
+        const uint32_t r0 = rec32[in ? e0 : 0];
+        return in ? r0 : su_pad<T>();
     };
 
     T st[G::NST];
     const uint32_t lane0 = lane * (uint32_t)(SU_LDP * sizeof(T));
-    uint2 sl_c = load_slot(0);
+    int bd_c = load_bounds(0);
+    int bd_n = nchunks > 1 ? load_bounds(1) : bd_c;
     if (!(SU_ABL & 4)) su_panel_load<T, YJ>(st, p, 0, j0, tid);
+    uint32_t rc_c = load_recs(bd_c);
     su_panel_store<T, YJ>(st, lds, c, tid);
     __syncthreads();
 
     for (int64_t ch = 0; ch < nchunks; ++ch) {
         const bool more = ch + 1 < nchunks;
-        uint2 sl_n = make_uint2(0u, 0u);
+        uint32_t rc_n = 0;
+        int bd_nn = bd_n;
         if (more) {
-            sl_n = load_slot(ch + 1);
+            rc_n = load_recs(bd_n);
             if (!(SU_ABL & 4)) su_panel_load<T, YJ>(st, p, ch + 1, j0, tid);
+            if (ch + 2 < nchunks) bd_nn = load_bounds(ch + 2);
         }
         const uint32_t lanex = lane0 + (uint32_t)((ch & 1) * G::PANEL * sizeof(T));
+        const int eb = __builtin_amdgcn_readlane(bd_c, 0);
+        const int ne = __builtin_amdgcn_readlane(bd_c, 1) - eb;
         if (!(SU_ABL & 1)) {
-            // rows' first two entries, SU_G rows at a time, software-pipelined: the reads of group
-            // g + 1 are issued before the adds of group g (sched_barrier keeps the compiler from
-            // hoisting every group's reads, which would need two registers per row)
-            constexpr int GG = sizeof(T) == 8 ? SU_G : 2 * SU_G;
-            auto reads = [&](int r, T &y0, T &y1, uint32_t &w) {
-                w = (uint32_t)__builtin_amdgcn_readlane((int)sl_c.x, r);
-                y0 = su_read<T>(lbase, lanex, w & 0x3fffu);
-                y1 = su_read<T>(lbase, lanex, (w >> 16) & 0x3fffu);
-            };
-            T ya[GG][2], yb[GG][2];
-            uint32_t wa[GG], wb[GG];
-#pragma unroll
-            for (int q = 0; q < GG; ++q) reads(q, ya[q][0], ya[q][1], wa[q]);
-#pragma unroll
-            for (int g = 0; g < SU_R; g += GG) {
-                const bool odd = (g / GG) & 1;
-                T (&cy)[GG][2] = odd ? yb : ya;
-                T (&ny)[GG][2] = odd ? ya : yb;
-                uint32_t (&cw)[GG] = odd ? wb : wa;
-                uint32_t (&nw)[GG] = odd ? wa : wb;
-                if (g + GG < SU_R) {
-#pragma unroll
-                    for (int q = 0; q < GG; ++q) reads(g + GG + q, ny[q][0], ny[q][1], nw[q]);
+            // Records in lane x of rc (lanes past the window hold padding; the walk reads at most
+            // 2 * SU_D - 1 past it): one readlane per entry, no branches. A range longer than one
+            // window (SU_WIN entries in 32 rows of one chunk, rare at C3) continues in further
+            // windows loaded from memory, through the same walk.
+            uint32_t rc = rc_c;
+            for (int done = 0; done < ne; done += SU_WIN) {
+                const int nw = ne - done < SU_WIN ? ne - done : SU_WIN;
+                if (done > 0) {
+                    const int e0 = eb + done + (int)lane;
+                    const uint32_t r0 = rec32[(int)lane < nw ? e0 : 0];
+                    rc = (int)lane < nw ? r0 : su_pad<T>();
                 }
-                __builtin_amdgcn_sched_barrier(0);
+                auto issue = [&](int x0, T (&y)[SU_D], uint32_t (&w)[SU_D]) {
 #pragma unroll
-                for (int q = 0; q < GG; ++q) {
-                    T s = acc[g + q] + su_flip<T>(cy[q][0], cw[q] << 16);
-                    s = s + su_flip<T>(cy[q][1], cw[q]);
-                    acc[g + q] = s;
-                    asm volatile("" : "+v"(acc[g + q]));   // the adds stay here, not sunk below
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-        if (!(SU_ABL & 2)) {
-            // rows with a third entry (about 8 % at C3): entries 3 and 4 from the slot word, in
-            // order; a fifth and later (0.4 %) from the CSR in memory
-            const uint64_t more3 = __builtin_amdgcn_ballot_w64((sl_c.y & 0xffffu) != su_absent<T>());
-            if (more3) {
-#pragma unroll
-                for (int r = 0; r < SU_R; ++r) {
-                    if ((more3 >> r) & 1u) {
-                        const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)sl_c.y, r);
-                        const T y2 = su_read<T>(lbase, lanex, w & 0x3fffu);
-                        const T y3 = su_read<T>(lbase, lanex, (w >> 16) & 0x3fffu);
-                        T s = acc[r] + su_flip<T>(y2, w << 16);
-                        s = s + su_flip<T>(y3, w);
-                        if (w & SU_MORE) {
-                            const int64_t v = ch * p.M + row0 + r;
-                            const int a = vrp[v], e = vrp[v + 1];
-#pragma unroll 1
-                            for (int x = a + 4; x < e; ++x) {
-                                const uint32_t q = rec16[x];
-                                s = s + su_flip<T>(su_read<T>(lbase, lanex, q & 0x3fffu), q << 16);
-                            }
-                        }
-                        acc[r] = s;
+                    for (int q = 0; q < SU_D; ++q) {
+                        w[q] = (uint32_t)__builtin_amdgcn_readlane((int)rc, x0 + q);
+                        if (SU_ABL & 16) y[q] = (T)(w[q] >> 8);   // diagnostics: no LDS read
+                        else y[q] = *reinterpret_cast<const T *>(lbase + lanex + ((w[q] >> 8) & 0x7ffu));
                     }
+                };
+                auto update = [&](const T (&y)[SU_D], const uint32_t (&w)[SU_D]) {
+#pragma unroll
+                    for (int q = 0; q < SU_D; ++q)
+                        acc.add_at(w[q], y[q]);
+                };
+                T ya[SU_D], yb[SU_D];
+                uint32_t wa[SU_D], wb[SU_D];
+                issue(0, ya, wa);
+                const int nsteps = (nw + SU_D - 1) / SU_D;
+#pragma unroll 1
+                for (int s2 = 0; s2 < nsteps; s2 += 2) {
+                    // step s2 (ya) has its reads in flight: issue step s2 + 1 (yb), then update
+                    issue((s2 + 1) * SU_D, yb, wb);
+                    update(ya, wa);
+                    if (s2 + 1 >= nsteps) break;
+                    issue((s2 + 2) * SU_D, ya, wa);
+                    update(yb, wb);
                 }
             }
         }
         if (more) su_panel_store<T, YJ>(st, lds + ((ch + 1) & 1) * G::PANEL, c, tid);
         __syncthreads();
-        sl_c = sl_n;
+        bd_c = bd_n;
+        bd_n = bd_nn;
+        rc_c = rc_n;
     }
 
     // epilogue
@@ -711,7 +718,7 @@ __global__ __launch_bounds__(SU_NT) void saso_unit_kernel(const SparseApply p, c
             T *reg = lds + (wave & 7) * SU_J * G::LDR;
             if (mine) {
 #pragma unroll
-                for (int r = 0; r < SU_R; ++r) reg[lane * G::LDR + r] = acc[r];
+                for (int r = 0; r < SU_R; ++r) reg[lane * G::LDR + r] = acc.get(r);
             }
             __syncthreads();
             if (mine) {
@@ -740,7 +747,7 @@ __global__ __launch_bounds__(SU_NT) void saso_unit_kernel(const SparseApply p, c
         T *cb = C + off;
 #pragma unroll
         for (int r = 0; r < SU_R; ++r)
-            if (row0 + r < p.M) cb[r * p.crs] = acc[r];
+            if (row0 + r < p.M) cb[r * p.crs] = acc.get(r);
     }
 }
 
@@ -767,7 +774,7 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
     err = rocprim::radix_sort_pairs(nullptr, tmp_bytes, k_in, k_out, v_in, v_out, n, 0, (unsigned)end_bit, s);
     if (err != hipSuccess) return err;
     const size_t bytes = 2 * n * sizeof(uint64_t) + 2 * n * sizeof(T) + (size_t)(NV + 1) * sizeof(int32_t) +
-                         2 * n * sizeof(uint16_t) + (size_t)(NV > 0 ? NV : 1) * sizeof(uint64_t) + sizeof(UniformTest<T>) +
+                         n * sizeof(uint16_t) + n * sizeof(uint32_t) + sizeof(UniformTest<T>) +
                          tmp_bytes + 512;
     char *ws = nullptr;
     err = hipMallocAsync((void **)&ws, bytes, s);
@@ -780,8 +787,7 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
     v_out = (T *)carve(n * sizeof(T));
     vrp = (int32_t *)carve((size_t)(NV + 1) * sizeof(int32_t));
     kl = (uint16_t *)carve(n * sizeof(uint16_t));
-    uint16_t *rec = (uint16_t *)carve(n * sizeof(uint16_t));
-    uint64_t *slot = (uint64_t *)carve((size_t)(NV > 0 ? NV : 1) * sizeof(uint64_t));
+    uint32_t *rec = (uint32_t *)carve(n * sizeof(uint32_t));
     UniformTest<T> *ut = (UniformTest<T> *)carve(sizeof(UniformTest<T>));
     tmp = carve(tmp_bytes);
 
@@ -803,17 +809,14 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
         if (err != hipSuccess) { (void)hipFreeAsync(ws, s); return err; }
     }
     hipLaunchKernelGGL(rowptr_kernel<T>, dim3((unsigned)((nnz + 1 + 255) / 256)), dim3(256), 0, s, nnz, k_out, v_out,
-                       NV, vrp, kl, rec);
-    if (unit && NV > 0)
-        hipLaunchKernelGGL(slot_kernel, dim3((unsigned)((NV + 255) / 256)), dim3(256), 0, s, NV, vrp, rec,
-                           su_absent<T>(), slot);
+                       NV, p.M, vrp, kl, rec);
     timing_begin(s);
     if (unit) {
         const int64_t nrb_u = (p.M + SU_ROWS - 1) / SU_ROWS;
         const dim3 grid_u((unsigned)(((p.N + SU_J - 1) / SU_J) * nrb_u));
         const int vec_out = p.crs == 1 && (p.ccs % VEC) == 0 && (((uintptr_t)p.C) % 16) == 0;
-        if (y_j) hipLaunchKernelGGL((saso_unit_kernel<T, true>), grid_u, dim3(SU_NT), 0, s, p, vrp, rec, slot, nchunks, nrb_u, ut, vec_out);
-        else hipLaunchKernelGGL((saso_unit_kernel<T, false>), grid_u, dim3(SU_NT), 0, s, p, vrp, rec, slot, nchunks, nrb_u, ut, vec_out);
+        if (y_j) hipLaunchKernelGGL((saso_unit_kernel<T, true>), grid_u, dim3(SU_NT), 0, s, p, vrp, rec, nchunks, nrb_u, ut, vec_out);
+        else hipLaunchKernelGGL((saso_unit_kernel<T, false>), grid_u, dim3(SU_NT), 0, s, p, vrp, rec, nchunks, nrb_u, ut, vec_out);
     }
     // general values (or a layout the kernel above does not take): exits at once when the
     // uniform-value kernel ran
