@@ -130,6 +130,26 @@ def test_lskges_apply_shapes(cuda, layout, opA, dtype, d, n, m, vec):
     check_left(cuda, layout, "N", opA, d, n, m, -2.0, 0.5, d, m, vec, "S", 8, 0, 0, dtype)
 
 
+@pytest.mark.parametrize("layout", ["C", "R"])
+@pytest.mark.parametrize("opS,opA", [("N", "N"), ("N", "T"), ("T", "N")])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("alpha,beta", [(1.0, 0.0), (-1.0, 0.5)])
+@pytest.mark.parametrize("d,n,m,vec,major", [(1000, 130, 2048, 8, "S"),   # ragged rows; 130 columns
+                                             (512, 64, 1024, 20, "S"),    # ~80 records per wave per chunk
+                                             (200, 72, 999, 3, "L"),      # LASO, K not a chunk multiple
+                                             (33, 8, 300, 2, "S")])       # one partial row block
+def test_lskges_unit_alpha_shapes(cuda, layout, opS, opA, dtype, alpha, beta, d, n, m, vec, major):
+    """Sampled operators with |alpha| = 1 (the uniform-value kernel with c = 1): bitwise against the
+    oracle, including dense chunks (multi-window waves), LASO and ragged shapes."""
+    SR, SC = (d, m) if opS == "N" else (m, d)
+    check_left(cuda, layout, opS, opA, d, n, m, alpha, beta, SR, SC, vec, major, 11, 0, 0, dtype)
+
+
+def test_lskges_config3_wide_slice(cuda):
+    """BASELINE config 3 at full height on 2048 columns: every 512-row block, all 128 chunks."""
+    check_left(cuda, "C", "N", "N", 1024, 2048, 16384, 1.0, 0.0, 1024, 16384, 8, "S", 0, 0, 0, np.float64)
+
+
 def test_lskges_config3_slice(cuda):
     """BASELINE config 3 operator (SASO d=1024, m=16384, vec_nnz=8) on a 64-column slice of A."""
     check_left(cuda, "C", "N", "N", 1024, 64, 16384, 1.0, 0.0, 1024, 16384, 8, "S", 0, 0, 0, np.float64)
