@@ -542,6 +542,7 @@ int sparse_common(SparseApply &p, const rbh_sparse_dist *D, const rbh_state *see
         T *gv = (T *)(gc + nnz);
         RBH_HIP(launch_fill_sparse_t<T>(make_sparse_gen(D, seed), gr, gc, gv, s));
         dr = gr; dc = gc; dv = gv;
+        p.unit_vals = 1;   // fill_sparse draws values +-1 (sparse_skops.hh:389-413)
     } else {
         RBH_REQUIRE(cols != nullptr && vals != nullptr && nnz >= 0);
         void *t0, *t1, *t2;

@@ -140,11 +140,11 @@ __global__ void coo_keys_kernel(int64_t nnz, const int64_t *rows, const int64_t 
 }
 
 // vrp[v] = first sorted position whose virtual row is >= v (invalid keys sort last); kl = k % SP_KC;
-// rec = the uniform-value apply's entry record (section 4): panel byte offset of k % SP_KC, the
-// accumulator register index of the row within its wave, sign of the value.
+// rec = the uniform-value apply's entry record (sections 4, 5): panel byte offset of k % SP_KC
+// (k * kmul), the accumulator register index of the row within its wave, sign of the value.
 template <typename T>
 __global__ void rowptr_kernel(int64_t nnz, const uint64_t *keys, const T *kv, int64_t NV, int64_t M, int32_t *vrp,
-                              uint16_t *kl, uint32_t *rec) {
+                              uint16_t *kl, uint32_t *rec, uint32_t kmul) {
     const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (e > nnz) return;
     const uint64_t inval = ~(uint64_t)0;
@@ -155,7 +155,7 @@ __global__ void rowptr_kernel(int64_t nnz, const uint64_t *keys, const T *kv, in
         const uint16_t k = (uint16_t)(keys[e] % SP_KC);
         kl[e] = k;
         const uint32_t row = (uint32_t)((keys[e] / SP_KC) % (uint64_t)M) % 32u;   // row within its wave
-        rec[e] = (sizeof(T) == 8 ? 2u * row : row) | ((uint32_t)(k * sizeof(T)) << 8) |
+        rec[e] = (sizeof(T) == 8 ? 2u * row : row) | (((uint32_t)k * kmul) << 8) |
                  (signbit(kv[e]) ? 0x80000000u : 0u);
     }
 }
@@ -775,6 +775,239 @@ __global__ __launch_bounds__(SU_NT) void saso_unit_kernel(const SparseApply p, c
     su_epilogue<T>(acc, lds, p, row0, j0, wave, lane, vec_out);
 }
 
+// ------------------------------------------------------------------------------------------
+// 5. Uniform-value apply with LDS-DMA staging (f64): sampled operators (values +-1) with
+//    |alpha| = 1, so P = Y exactly. The walk is section 4's, but nothing is loaded into VGPRs
+//    while it runs: the next chunk's panel and CSR records, and the row bounds of the chunk after,
+//    are copied global -> LDS with global_load_lds (no VGPR destination), issued before the walk
+//    and drained at the chunk's barrier, so the copies overlap the walk (section 4's loads must
+//    complete before GPR index mode is switched on).
+//    Panel layouts, unpadded; the walk address is lane_base ^ koff:
+//      * Y contiguous along k (YJ = false): [64 columns][SP_KC]; 16-B vector v of column c sits in
+//        slot v ^ (c & 15), which spreads the 64 lanes' reads of one k over the banks;
+//        koff = k * sizeof(T).
+//      * Y contiguous along j (YJ = true): [SP_KC][64 columns]; koff = k * 64 * sizeof(T).
+//    Padding records add into a dummy accumulator register (v[96:97]), so no zero element.
+//    The workgroup's records of a chunk are one contiguous CSR range; up to SD_RCAP of them are
+//    staged (mean at C3: 512), the rest are read from HBM before their window.
+// ------------------------------------------------------------------------------------------
+constexpr int SD_RCAP = 2048;
+
+template <typename T> struct SdCfg {
+    static constexpr int VEC = 16 / (int)sizeof(T);
+    static constexpr int PANEL_B = SP_KC * SU_J * (int)sizeof(T);   // bytes per panel buffer
+    static constexpr int REC_OFF = 2 * PANEL_B;
+    static constexpr int BND_OFF = REC_OFF + 2 * SD_RCAP * 4;
+    static constexpr int MAIN_B = BND_OFF + 4 * 64 * 4;
+    static constexpr int EPI_B = SuCfg<T>::EPI * (int)sizeof(T);
+    static constexpr int BYTES = MAIN_B > EPI_B ? MAIN_B : EPI_B;
+    static constexpr uint32_t PAD = 64u;   // padding record: the dummy's register index, koff 0, sign +
+};
+
+// SuAcc<double> plus the dummy register v[96:97] the padding records add into.
+struct SdAcc {
+    typedef double v16 __attribute__((ext_vector_type(16)));
+    v16 a, b;
+    double dmy;
+    __device__ __forceinline__ double get(int r) const { return r < 16 ? a[r] : b[r - 16]; }
+    __device__ __forceinline__ void set(int r, double x) { if (r < 16) a[r] = x; else b[r - 16] = x; }
+    __device__ __forceinline__ void add_at(uint32_t rec, double y) {
+        uint32_t m;
+        asm("s_and_b32 %0, %1, 0x80000000" : "=s"(m) : "s"(rec) : "scc");
+        const double ys = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, y) ^ ((uint64_t)m << 32));
+        asm volatile("s_waitcnt lgkmcnt(0)\n\t"
+                     "s_set_gpr_idx_on %3, gpr_idx(SRC0,DST)\n\t"
+                     "v_add_f64 v[32:33], v[32:33], %4\n\t"
+                     "s_set_gpr_idx_off"
+                     : "+{v[32:63]}"(a), "+{v[64:95]}"(b), "+{v[96:97]}"(dmy)
+                     : "s"(rec), "v"(ys)
+                     : "m0", "scc");
+    }
+};
+
+__device__ __forceinline__ uint32_t lds_addr(const void *ptr) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)ptr;
+}
+// global -> LDS copies: lane l's 16 (4) bytes from g land at LDS byte m0 + 16 l (4 l). M0 is set in
+// the same statement, because the walk's s_set_gpr_idx_on overwrites it.
+__device__ __forceinline__ void dma16(const void *g, uint32_t m0) {
+    asm volatile("s_mov_b32 m0, %0\n\t"
+                 "global_load_lds_dwordx4 %1, off"
+                 :
+                 : "s"(m0), "v"(g)
+                 : "memory", "m0");
+}
+__device__ __forceinline__ void dma4(const void *g, uint32_t m0) {
+    asm volatile("s_mov_b32 m0, %0\n\t"
+                 "global_load_lds_dword %1, off"
+                 :
+                 : "s"(m0), "v"(g)
+                 : "memory", "m0");
+}
+
+template <bool YJ>
+__global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, const int32_t *vrp,
+                                                         const uint32_t *rec32, int64_t nchunks, int64_t nrb,
+                                                         int vec_out) {
+    typedef double T;
+    typedef SdCfg<T> G;
+    constexpr int VEC = G::VEC;
+    __shared__ __attribute__((aligned(16))) char smem[G::BYTES];
+    const char *lbase = smem;
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
+    const uint32_t *recs = reinterpret_cast<const uint32_t *>(smem + G::REC_OFF);
+    const int32_t *bnd = reinterpret_cast<const int32_t *>(smem + G::BND_OFF);
+
+    const int tid = threadIdx.x;
+    const uint32_t lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t nb = (int64_t)gridDim.x;
+    const int64_t b = blockIdx.x;
+    const int64_t xcd = b % 8, qq = nb / 8, rr = nb % 8;
+    const int64_t t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + b / 8;
+    const int64_t rb0 = (t % nrb) * SU_ROWS;
+    const int64_t j0 = (t / nrb) * SU_J;
+    const int64_t row0 = rb0 + (int64_t)wave * SU_R;
+    const int64_t j = j0 + lane;
+    const bool jin = j < p.N;
+    const T *Y = (const T *)p.Y;
+    const T beta = (T)p.beta;
+
+    SdAcc acc;
+    acc.dmy = (T)0;
+    if (beta != (T)0) {
+        int64_t off = row0 * p.crs + j * p.ccs;
+        asm volatile("" : "+v"(off));
+        const T *cb = (const T *)p.C + off;
+#pragma unroll
+        for (int r = 0; r < SU_R; ++r) acc.set(r, (jin && row0 + r < p.M) ? beta * cb[r * p.crs] : (T)0);
+    } else {
+#pragma unroll
+        for (int r = 0; r < SU_R; ++r) acc.set(r, (T)0);
+    }
+
+    // row bounds of chunk cc: bnd[(cc & 3) * 64 + l] = start of wave l's rows, l <= 16 (l = 16: end)
+    auto dma_bounds = [&](int64_t cc) {
+        if (wave == 0) {
+            const int64_t l = lane < 16 ? lane : 16;
+            const int64_t r = rb0 + SU_R * l < p.M ? rb0 + SU_R * l : p.M;
+            dma4(vrp + cc * p.M + r, lds0 + G::BND_OFF + (uint32_t)((cc & 3) * 256));
+        }
+    };
+    // panel of chunk cc -> buffer cc & 1; 1 KB per instruction, out-of-range sources clamped (the
+    // elements they bring are never read: no record points at k >= K, columns >= N are not stored)
+    auto dma_panel = [&](int64_t cc) {
+        const uint32_t pb = lds0 + (uint32_t)((cc & 1) * G::PANEL_B);
+        const int64_t kc0 = cc * SP_KC;
+        if (!YJ) {
+            constexpr int COLB = SP_KC * (int)sizeof(T);   // bytes per column
+            constexpr int CPI = 1024 / COLB;              // columns per instruction
+            constexpr int SPC = COLB / 16;                // 16-B slots per column
+            constexpr int NI = SU_J / CPI / 16;           // instructions per wave
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const int inst = wave * NI + i;
+                const int col = inst * CPI + (int)lane / SPC;
+                const int v = ((int)lane % SPC) ^ (col & 15);
+                const int64_t gj = j0 + col < p.N ? j0 + col : p.N - 1;
+                const int64_t gk = kc0 + VEC * v < p.K ? kc0 + VEC * v : 0;
+                dma16(Y + gj * p.ysj + gk, pb + (uint32_t)(inst * 1024));
+            }
+        } else {
+            constexpr int RB = SU_J * (int)sizeof(T);     // bytes per panel row
+            constexpr int RPI = 1024 / RB;                // rows per instruction
+            constexpr int VPR = RB / 16;                  // 16-B vectors per row
+            constexpr int NI = SP_KC / RPI / 16;          // instructions per wave
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const int inst = wave * NI + i;
+                const int64_t gk = kc0 + inst * RPI + (int)lane / VPR < p.K ? kc0 + inst * RPI + (int)lane / VPR : 0;
+                const int64_t gj = j0 + VEC * ((int)lane % VPR) < p.N ? j0 + VEC * ((int)lane % VPR) : 0;
+                dma16(Y + gk * p.ysk + gj, pb + (uint32_t)(inst * 1024));
+            }
+        }
+    };
+    // the workgroup's records of chunk cc (bounds already in LDS) -> recs[(cc & 1) * SD_RCAP ..]
+    auto dma_recs = [&](int64_t cc) {
+        const int32_t *bb = bnd + (cc & 3) * 64;
+        const int B0 = __builtin_amdgcn_readfirstlane(bb[0]), B1 = __builtin_amdgcn_readfirstlane(bb[16]);
+        const int n = B1 - B0 < SD_RCAP ? B1 - B0 : SD_RCAP;
+        for (int q = wave; q * 64 < n; q += 16) {
+            const int e = B0 + q * 64 + (int)lane;
+            dma4(rec32 + (e < B1 ? e : B0), lds0 + G::REC_OFF + (uint32_t)(((cc & 1) * SD_RCAP + q * 64) * 4));
+        }
+    };
+
+    dma_bounds(0);
+    if (nchunks > 1) dma_bounds(1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    dma_recs(0);
+    dma_panel(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    const uint32_t lanebase = YJ ? lane * (uint32_t)sizeof(T)
+                                 : lane * (uint32_t)(SP_KC * sizeof(T)) + 16u * (lane & 15u);
+    for (int64_t ch = 0; ch < nchunks; ++ch) {
+        if (ch + 1 < nchunks) {
+            dma_recs(ch + 1);
+            dma_panel(ch + 1);
+        }
+        if (ch + 2 < nchunks) dma_bounds(ch + 2);
+        const int32_t *bb = bnd + (ch & 3) * 64;
+        const int B0 = __builtin_amdgcn_readfirstlane(bb[0]);
+        const int eb = __builtin_amdgcn_readfirstlane(bb[wave]) - B0;
+        int ne = __builtin_amdgcn_readfirstlane(bb[wave + 1]) - B0 - eb;
+        // a sampled operator has no duplicate (row, k): at most SU_R * SP_KC entries per wave
+        ne = ne < 0 ? 0 : (ne > SU_R * SP_KC ? SU_R * SP_KC : ne);
+        const uint32_t L = lanebase + (uint32_t)((ch & 1) * G::PANEL_B);
+        const uint32_t *rbuf = recs + (ch & 1) * SD_RCAP;
+        auto walk = [&](uint32_t rc, int nw) {
+            auto issue = [&](int x0, T (&y)[SU_D], uint32_t (&w)[SU_D]) {
+#pragma unroll
+                for (int q = 0; q < SU_D; ++q) {
+                    w[q] = (uint32_t)__builtin_amdgcn_readlane((int)rc, x0 + q);
+                    y[q] = *reinterpret_cast<const T *>(lbase + (L ^ ((w[q] >> 8) & 0xfffffu)));
+                }
+            };
+            auto update = [&](const T (&y)[SU_D], const uint32_t (&w)[SU_D]) {
+#pragma unroll
+                for (int q = 0; q < SU_D; ++q) acc.add_at(w[q], y[q]);
+            };
+            T ya[SU_D], yb[SU_D];
+            uint32_t wa[SU_D], wb[SU_D];
+            issue(0, ya, wa);
+            const int nsteps = (nw + SU_D - 1) / SU_D;
+#pragma unroll 1
+            for (int s2 = 0; s2 < nsteps; s2 += 2) {
+                issue((s2 + 1) * SU_D, yb, wb);
+                update(ya, wa);
+                if (s2 + 1 >= nsteps) break;
+                issue((s2 + 2) * SU_D, ya, wa);
+                update(yb, wb);
+            }
+        };
+        for (int done = 0; done < ne; done += SU_WIN) {
+            const int nw = ne - done < SU_WIN ? ne - done : SU_WIN;
+            const int rel = eb + done + (int)lane;
+            uint32_t rc;
+            if (eb + done + nw <= SD_RCAP) {
+                const uint32_t x = rbuf[rel < SD_RCAP ? rel : 0];
+                rc = (int)lane < nw ? x : G::PAD;
+            } else {   // past the staged records (rare): from HBM, complete before the walk
+                const uint32_t x = rec32[B0 + ((int)lane < nw ? rel : eb)];
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                rc = (int)lane < nw ? x : G::PAD;
+            }
+            walk(rc, nw);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    su_epilogue<T>(acc, reinterpret_cast<T *>(smem), p, row0, j0, wave, lane, vec_out);
+}
+
 template <typename T>
 static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, const int64_t *cols, const T *vals,
                                      int64_t nnz, hipStream_t s) {
@@ -823,20 +1056,37 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
     // f64 only: the f32 instantiation (index-mode v_add_f32) still loses entries on gfx950 with
     // nothing in flight, cause not found; f32 takes the general-value kernel
     const bool unit = (y_j || y_k) && !unit_off && sizeof(T) == 8;
+    // LDS-DMA kernel (section 5): f64, values +-1 (operator sampled in this call), |alpha| = 1
+    static const bool dma_off = [] { const char *e = getenv("RBH_NO_SASO_DMA"); return e && e[0] == '1'; }();
+    const bool y_jd = p.ysj == 1 && (p.ysk % VEC) == 0 && (((uintptr_t)p.Y) % 16) == 0 && (p.N % VEC) == 0;
+    const bool dma = sizeof(T) == 8 && p.unit_vals && (p.alpha == 1.0 || p.alpha == -1.0) && (y_k || y_jd) &&
+                     !dma_off;
+    const uint32_t kmul = (dma && !y_k) ? (uint32_t)(SU_J * sizeof(T)) : (uint32_t)sizeof(T);
     err = hipMemsetAsync(ut, 0, sizeof(UniformTest<T>), s);
     if (err != hipSuccess) { (void)hipFreeAsync(ws, s); return err; }
 
     if (nnz > 0) {
         hipLaunchKernelGGL(coo_keys_kernel<T>, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, rows, cols,
                            vals, p.ro, p.co, p.win_r, p.win_c, p.transposed, p.M, (T)p.alpha, k_in, v_in,
-                           unit ? ut : nullptr);
+                           (unit && !dma) ? ut : nullptr);
         // invalid keys (~0) still sort last: their low end_bit bits are all ones, above every valid key
         err = rocprim::radix_sort_pairs(tmp, tmp_bytes, k_in, k_out, v_in, v_out, (size_t)nnz, 0, (unsigned)end_bit, s);
         if (err != hipSuccess) { (void)hipFreeAsync(ws, s); return err; }
     }
     hipLaunchKernelGGL(rowptr_kernel<T>, dim3((unsigned)((nnz + 1 + 255) / 256)), dim3(256), 0, s, nnz, k_out, v_out,
-                       NV, p.M, vrp, kl, rec);
+                       NV, p.M, vrp, kl, rec, kmul);
     timing_begin(s);
+    if (dma) {
+        const int64_t nrb_u = (p.M + SU_ROWS - 1) / SU_ROWS;
+        const dim3 grid_u((unsigned)(((p.N + SU_J - 1) / SU_J) * nrb_u));
+        const int vec_out = p.crs == 1 && (p.ccs % VEC) == 0 && (((uintptr_t)p.C) % 16) == 0;
+        if (y_k) hipLaunchKernelGGL((saso_dma_kernel<false>), grid_u, dim3(SU_NT), 0, s, p, vrp, rec, nchunks, nrb_u, vec_out);
+        else hipLaunchKernelGGL((saso_dma_kernel<true>), grid_u, dim3(SU_NT), 0, s, p, vrp, rec, nchunks, nrb_u, vec_out);
+        err = hipGetLastError();
+        timing_end(s);
+        hipError_t e2 = hipFreeAsync(ws, s);
+        return err != hipSuccess ? err : e2;
+    }
     if (unit) {
         const int64_t nrb_u = (p.M + SU_ROWS - 1) / SU_ROWS;
         const dim3 grid_u((unsigned)(((p.N + SU_J - 1) / SU_J) * nrb_u));
