@@ -6,6 +6,7 @@
 //   DenseDistName / DenseDist / DenseSkOp (dense_skops.hh:204-419), fill_dense x3 (:486-592),
 //   SparseDist / SparseSkOp / fill_sparse (sparse_skops.hh:134-413),
 //   sketch_general x8 (skge.hh:771-1214), sketch_symmetric x4 (sksy.hh:165-537),
+//   sketch_vector x2 (skve.hh:152-258),
 //   exceptions::Error (exceptions.hh:45-70), and the blas::Layout / blas::Op enums of BLAS++,
 // and routes every call to the MI355X C ABI (include/randblas_hip.h). Host arrays work as in
 // the reference (they are staged through HBM; the call is synchronous); device arrays
@@ -496,6 +497,24 @@ inline void sketch_symmetric(blas::Layout layout, T alpha, SKOP &S, const T *A, 
     util::require_symmetric(layout, A, n, lda, sym_check_tol);
     sketch_general(layout, blas::Op::NoTrans, blas::Op::NoTrans, d, n, n, alpha, S, (int64_t)0, (int64_t)0, A, lda,
                    beta, B, ldb);
+}
+
+// ---------------------------------------------------------------------------------------------
+// sketch_vector (skve.hh:152-258): sketch_general in RowMajor with n = 1, lda = incx, ldb = incy
+// ---------------------------------------------------------------------------------------------
+// y = alpha op(submat(S)) x + beta y, with submat(S) of size d x m (before op)
+template <typename T, typename SKOP>
+inline void sketch_vector(blas::Op opS, int64_t d, int64_t m, T alpha, SKOP &S, int64_t ro_s, int64_t co_s,
+                          const T *x, int64_t incx, T beta, T *y, int64_t incy) {
+    const int64_t dd = opS == blas::Op::NoTrans ? d : m, mm = opS == blas::Op::NoTrans ? m : d;
+    sketch_general(blas::Layout::RowMajor, opS, blas::Op::NoTrans, dd, (int64_t)1, mm, alpha, S, ro_s, co_s, x, incx,
+                   beta, y, incy);
+}
+
+// y = alpha op(S) x + beta y over the whole operator (skve.hh:244-258)
+template <typename T, typename SKOP>
+inline void sketch_vector(blas::Op opS, T alpha, SKOP &S, const T *x, int64_t incx, T beta, T *y, int64_t incy) {
+    sketch_vector(opS, S.dist.n_rows, S.dist.n_cols, alpha, S, (int64_t)0, (int64_t)0, x, incx, beta, y, incy);
 }
 
 }  // namespace RandBLAS

@@ -175,6 +175,31 @@ static void symmetric_and_errors() {
     CHECK(threw);
 }
 
+static void vector_sketch() {
+    // test_sketch_vector.cc: wide 100 x 1000 (incx 2, incy 3) and the transposed tall operator
+    const int64_t d = 100, m = 1000, incx = 2, incy = 3;
+    std::vector<double> x(incx * m, 0.0);
+    for (int64_t i = 0; i < m; ++i) x[incx * i] = 1.0;
+    RandBLAS::DenseDist Dw(d, m), Dt(m, d);
+    RandBLAS::DenseSkOp<double> Sw(Dw, 1), St(Dt, 1);
+    std::vector<double> yw(incy * d, 0.0), yt(incy * d, 0.0);
+    RandBLAS::sketch_vector(Op::NoTrans, d, m, 1.0, Sw, 0, 0, x.data(), incx, 0.0, yw.data(), incy);
+    RandBLAS::sketch_vector(Op::Trans, 1.0, St, x.data(), incx, 0.0, yt.data(), incy);
+    std::vector<double> Se(d * m);
+    RandBLAS::fill_dense(Layout::RowMajor, Dw, d, m, 0, 0, Se.data(), Sw.seed_state);
+    const double eps = std::numeric_limits<double>::epsilon();
+    for (int64_t i = 0; i < d; ++i) {
+        double ex = 0, bound = 0;
+        for (int64_t k = 0; k < m; ++k) {
+            ex += Se[i * m + k];
+            bound += std::fabs(Se[i * m + k]);
+        }
+        bound *= (double)m * 2 * eps;
+        CHECK(std::fabs(yw[incy * i] - ex) <= bound);
+        CHECK(std::fabs(yt[incy * i] - ex) <= 2 * bound);
+    }
+}
+
 int main() {
     dense_left<double>(Layout::ColMajor);
     dense_left<double>(Layout::RowMajor);
@@ -182,6 +207,7 @@ int main() {
     dense_submatrix_and_right();
     sparse_left();
     symmetric_and_errors();
+    vector_sketch();
     if (g_fail) {
         std::printf("%d checks FAILED\n", g_fail);
         return 1;
