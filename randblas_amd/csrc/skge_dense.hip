@@ -455,7 +455,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void skge_fused_kernel(cons
     const int g4 = (lane >> 4) * 4;
     const int r = lane & 15;
 
-    // The two waves sharing a SIMD (waves w and w + 4) run the step's two phases in opposite
+    // Waves sharing a SIMD (w, w + 4, ...) alternate the step's two phases in opposite
     // order -- one does its MFMAs while the other draws the next tile's samples -- so the matrix
     // pipe of the SIMD is fed while the VALU works on the draw.
     // (Two copies of the whole loop rather than a branch inside it: register allocation then sees
@@ -489,7 +489,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void skge_fused_kernel(cons
             __syncthreads();
         }
     };
-    if (__builtin_amdgcn_readfirstlane(wave) < 4) k_loop(std::true_type{});
+    if (((__builtin_amdgcn_readfirstlane(wave) >> 2) & 1) == 0) k_loop(std::true_type{});
     else k_loop(std::false_type{});
 
     T *C = (T *)p.C;
@@ -820,13 +820,23 @@ static hipError_t launch_gemm(const GemmProblem &p, hipStream_t s) {
 #undef RBH_WIDE_L
     }
     if (fused_ok(p)) {
+        // tile (generated x memory outer indices) and waves; f32 variants selectable for tuning
+#ifndef RBH_F32_TG
+#define RBH_F32_TG 128
+#define RBH_F32_TM 256
+#define RBH_F32_WG 2
+#define RBH_F32_WMW 4
+#endif
+        constexpr bool F32 = sizeof(T) == 4;
+        constexpr int TG = F32 ? RBH_F32_TG : 128, TMW = F32 ? RBH_F32_TM : 256;
+        constexpr int WG = F32 ? RBH_F32_WG : 2, WMW = F32 ? RBH_F32_WMW : 4;
 #define RBH_FUSED(XK, YK, BM, BN, WMS, WNS)                                                    \
     return unif ? launch_fused<T, XK, YK, rb::UNIFORM, BM, BN, WMS, WNS>(p, s)                  \
                 : launch_fused<T, XK, YK, rb::GAUSSIAN, BM, BN, WMS, WNS>(p, s)
-        if (p.xkind == GEN_OK) { RBH_FUSED(GEN_OK, MEM, 128, 256, 2, 4); }
-        if (p.xkind == GEN_OO) { RBH_FUSED(GEN_OO, MEM, 128, 256, 2, 4); }
-        if (p.ykind == GEN_OK) { RBH_FUSED(MEM, GEN_OK, 256, 128, 4, 2); }
-        if (p.ykind == GEN_OO) { RBH_FUSED(MEM, GEN_OO, 256, 128, 4, 2); }
+        if (p.xkind == GEN_OK) { RBH_FUSED(GEN_OK, MEM, TG, TMW, WG, WMW); }
+        if (p.xkind == GEN_OO) { RBH_FUSED(GEN_OO, MEM, TG, TMW, WG, WMW); }
+        if (p.ykind == GEN_OK) { RBH_FUSED(MEM, GEN_OK, TMW, TG, WMW, WG); }
+        if (p.ykind == GEN_OO) { RBH_FUSED(MEM, GEN_OO, TMW, TG, WMW, WG); }
 #undef RBH_FUSED
     }
 #define RBH_FAM(XK, YK, BM, BN, WMS, WNS)                                                    \
