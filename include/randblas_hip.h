@@ -140,6 +140,40 @@ int rbh_rskges_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_
                    const int64_t *rows, const int64_t *cols, const float *vals, int64_t ro_s, int64_t co_s,
                    float beta, float *B, int64_t ldb, void *stream);
 
+/* sketch_sparse: dense operator x sparse data matrix (RandBLAS/sparse_data/sksp.hh).
+ * The data matrix A is passed as (A_fmt, A_rows, A_cols, A_nnz, A_p, A_i, A_v):
+ *   A_fmt 'O' COOMatrix (coo_matrix.hh): A_p = rows, A_i = cols;
+ *   A_fmt 'R' CSRMatrix (csr_matrix.hh): A_p = rowptr (A_rows + 1), A_i = colidxs;
+ *   A_fmt 'C' CSCMatrix (csc_matrix.hh): A_p = colptr (A_cols + 1), A_i = rowidxs;
+ * int64 indices, A_v the values. The dense operator is (D, seed) with optional explicit S_buff in
+ * S_layout, as for rbh_lskge3. Each entry of B accumulates in ascending contracted index with
+ * separate multiply and add; the reference's CSR/CSC kernels use other orders (axpy), so parity
+ * is within the reference's componentwise bound.
+ * Left (sparse_data::lsksp3, sksp.hh:147-192; sketch_sparse, :464-485):
+ *   B = alpha * op(submat(S)) * op(submat(A)) + beta * B, B d x n. */
+int rbh_lsksp3_f64(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, double alpha,
+                   const rbh_dense_dist *D, const rbh_state *seed, const double *S_buff, char S_layout, int64_t ro_s,
+                   int64_t co_s, char A_fmt, int64_t A_rows, int64_t A_cols, int64_t A_nnz, const int64_t *A_p,
+                   const int64_t *A_i, const double *A_v, int64_t ro_a, int64_t co_a, double beta, double *B,
+                   int64_t ldb, void *stream);
+int rbh_lsksp3_f32(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, float alpha,
+                   const rbh_dense_dist *D, const rbh_state *seed, const float *S_buff, char S_layout, int64_t ro_s,
+                   int64_t co_s, char A_fmt, int64_t A_rows, int64_t A_cols, int64_t A_nnz, const int64_t *A_p,
+                   const int64_t *A_i, const float *A_v, int64_t ro_a, int64_t co_a, float beta, float *B,
+                   int64_t ldb, void *stream);
+/* Right (sparse_data::rsksp3, sksp.hh:302-350; sketch_sparse, :595-615):
+ *   B = alpha * op(submat(A)) * op(submat(S)) + beta * B, B m x d. */
+int rbh_rsksp3_f64(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, double alpha, char A_fmt,
+                   int64_t A_rows, int64_t A_cols, int64_t A_nnz, const int64_t *A_p, const int64_t *A_i,
+                   const double *A_v, int64_t ro_a, int64_t co_a, const rbh_dense_dist *D, const rbh_state *seed,
+                   const double *S_buff, char S_layout, int64_t ro_s, int64_t co_s, double beta, double *B,
+                   int64_t ldb, void *stream);
+int rbh_rsksp3_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, float alpha, char A_fmt,
+                   int64_t A_rows, int64_t A_cols, int64_t A_nnz, const int64_t *A_p, const int64_t *A_i,
+                   const float *A_v, int64_t ro_a, int64_t co_a, const rbh_dense_dist *D, const rbh_state *seed,
+                   const float *S_buff, char S_layout, int64_t ro_s, int64_t co_s, float beta, float *B, int64_t ldb,
+                   void *stream);
+
 /* ---- sketch_symmetric support ------------------------------------------------------------- */
 /* util::require_symmetric (util.hh:165-188) on the device: RBH_OK if |A_ij - A_ji| <=
  * (|A_ij| + |A_ji| + 1) * tol for all i < j (tol < 0 skips the check), else RBH_ERR_SYMMETRY.

@@ -97,6 +97,12 @@ for _t, _ct in (("f64", ctypes.c_double), ("f32", ctypes.c_float)):
                                                  P(SparseDistC), P(RNGStateC), c_i64, c_vp, c_vp, c_vp, c_i64, c_i64,
                                                  _ct, c_vp, c_i64, c_vp]
     getattr(lib, f"rbh_require_symmetric_{_t}").argtypes = [c_char, c_vp, c_i64, c_i64, _ct, c_vp]
+    _spm = [c_char, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64]   # A_fmt .. co_a
+    _dop = [P(DenseDistC), P(RNGStateC), c_vp, c_char, c_i64, c_i64]       # D .. co_s
+    getattr(lib, f"rbh_lsksp3_{_t}").argtypes = [c_char, c_char, c_char, c_i64, c_i64, c_i64, _ct] + _dop + _spm + \
+        [_ct, c_vp, c_i64, c_vp]
+    getattr(lib, f"rbh_rsksp3_{_t}").argtypes = [c_char, c_char, c_char, c_i64, c_i64, c_i64, _ct] + _spm + _dop + \
+        [_ct, c_vp, c_i64, c_vp]
 
 # --------------------------------------------------------------------------------------------
 # Python mirror of the reference's types
@@ -361,6 +367,94 @@ def sketch_vector_full(opS, alpha, S, x, incx, beta, y, incy, stream=None):
     sketch_vector(opS, S.dist.n_rows, S.dist.n_cols, alpha, S, x, incx, beta, y, incy, 0, 0, stream)
 
 
+# --------------------------------------------------------------------------------------------
+# sketch_sparse: dense operator x sparse data (RandBLAS/sparse_data/sksp.hh)
+# --------------------------------------------------------------------------------------------
+@dataclass
+class COOMatrix:
+    """COOMatrix (sparse_data/coo_matrix.hh): nnz entries (rows[e], cols[e], vals[e]), int64 indices."""
+
+    n_rows: int
+    n_cols: int
+    rows: object
+    cols: object
+    vals: object
+    nnz: Optional[int] = None
+    _fmt = "O"
+
+    def _arrays(self):
+        return self.rows, self.cols
+
+
+@dataclass
+class CSRMatrix:
+    """CSRMatrix (sparse_data/csr_matrix.hh): rowptr (n_rows + 1), colidxs, vals; int64 indices."""
+
+    n_rows: int
+    n_cols: int
+    rowptr: object
+    colidxs: object
+    vals: object
+    nnz: Optional[int] = None
+    _fmt = "R"
+
+    def _arrays(self):
+        return self.rowptr, self.colidxs
+
+
+@dataclass
+class CSCMatrix:
+    """CSCMatrix (sparse_data/csc_matrix.hh): colptr (n_cols + 1), rowidxs, vals; int64 indices."""
+
+    n_rows: int
+    n_cols: int
+    colptr: object
+    rowidxs: object
+    vals: object
+    nnz: Optional[int] = None
+    _fmt = "C"
+
+    def _arrays(self):
+        return self.colptr, self.rowidxs
+
+
+def _spm_args(A):
+    p_arr, i_arr = A._arrays()
+    nnz = A.nnz if A.nnz is not None else len(A.vals)
+    return [_b(A._fmt), A.n_rows, A.n_cols, nnz, _ptr(p_arr), _ptr(i_arr), _ptr(A.vals)]
+
+
+def _dense_op_args(S, ro_s, co_s):
+    if not isinstance(S, DenseSkOp):
+        raise TypeError("sketch_sparse takes a DenseSkOp")
+    return [ctypes.byref(S.dist.c()), ctypes.byref(S.seed_state.c()), _ptr(S.buff), _b(S.buff_layout), ro_s, co_s]
+
+
+def sketch_sparse_left(layout, opS, opA, d, n, m, alpha, S, A, beta, B, ldb, ro_s=0, co_s=0, ro_a=0, co_a=0,
+                       stream=None):
+    """B = alpha op(submat(S)) op(submat(A)) + beta B with A sparse (sparse_data::lsksp3, sksp.hh:147-192)."""
+    t = _dtype_tag(B)
+    fn = getattr(lib, f"rbh_lsksp3_{t}")
+    _check(fn(_b(layout), _b(opS), _b(opA), d, n, m, alpha, *_dense_op_args(S, ro_s, co_s), *_spm_args(A), ro_a,
+              co_a, beta, _ptr(B), ldb, _stream(B, stream)))
+
+
+def sketch_sparse_right(layout, opA, opS, m, d, n, alpha, A, S, beta, B, ldb, ro_a=0, co_a=0, ro_s=0, co_s=0,
+                        stream=None):
+    """B = alpha op(submat(A)) op(submat(S)) + beta B with A sparse (sparse_data::rsksp3, sksp.hh:302-350)."""
+    t = _dtype_tag(B)
+    fn = getattr(lib, f"rbh_rsksp3_{t}")
+    _check(fn(_b(layout), _b(opA), _b(opS), m, d, n, alpha, *_spm_args(A), ro_a, co_a, *_dense_op_args(S, ro_s, co_s),
+              beta, _ptr(B), ldb, _stream(B, stream)))
+
+
+def sketch_sparse(layout, op1, op2, d_or_m, n_or_d, m_or_n, alpha, X, Y, *args, **kw):
+    """Overload dispatcher mirroring RandBLAS::sketch_sparse: left form when X is the DenseSkOp."""
+    if isinstance(X, DenseSkOp):
+        return sketch_sparse_left(layout, op1, op2, d_or_m, n_or_d, m_or_n, alpha, X, Y, *args, **kw)
+    return sketch_sparse_right(layout, op1, op2, d_or_m, n_or_d, m_or_n, alpha, X, Y, *args, **kw)
+
+
 def kernel_timing(on: bool) -> None:
     """Enable/disable HIP-event timing of each call's dominant kernel (diagnostics)."""
     lib.rbh_kernel_timing_enable(1 if on else 0)
@@ -381,5 +475,6 @@ __all__ = [
     "RNGState", "DenseDist", "SparseDist", "DenseSkOp", "SparseSkOp", "RandBLASError", "fill_dense", "fill_sparse",
     "sketch_general", "sketch_general_left", "sketch_general_right", "sketch_symmetric_left",
     "sketch_symmetric_right", "require_symmetric", "dense_next_state", "sparse_next_state", "abi_version", "lib",
-    "LIB_PATH", "kernel_timing", "kernel_times_ms", "sketch_vector", "sketch_vector_full",
+    "LIB_PATH", "kernel_timing", "kernel_times_ms", "sketch_vector", "sketch_vector_full", "COOMatrix",
+    "CSRMatrix", "CSCMatrix", "sketch_sparse", "sketch_sparse_left", "sketch_sparse_right",
 ]

@@ -625,6 +625,166 @@ int rskges(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, T a
                             extent(layout, m, d, ldb), beta, (hipStream_t)stream);
 }
 
+// ---------------------------------------------------------------------------------------------
+// sketch_sparse: dense operator x sparse data matrix (sparse_data/sksp.hh:147-330, 464-615).
+// As the reference does for an unfilled S (submatrix_as_blackbox, sksp.hh:168-172), submat(S) is
+// materialised (device fill); the product is then the sparse apply of saso.hip with the data
+// matrix as the sparse operand and submat(S) as the dense one.
+// ---------------------------------------------------------------------------------------------
+// The data matrix as device COO arrays. Formats: 'O' COO (p = rows, i = cols), 'R' CSR (p = rowptr,
+// n_rows + 1 entries; i = colidxs), 'C' CSC (p = colptr, n_cols + 1; i = rowidxs). int64 indices
+// (the reference's default sint_t). CSR/CSC pointers are expanded on the device into *ws.
+template <typename T>
+int data_as_coo(Stager &st, char fmt, int64_t n_rows, int64_t n_cols, int64_t nnz, const int64_t *A_p,
+                const int64_t *A_i, const T *A_v, const int64_t **rows, const int64_t **cols, const T **vals,
+                void **ws, hipStream_t s) {
+    *ws = nullptr;
+    *rows = *cols = nullptr;
+    *vals = nullptr;
+    RBH_REQUIRE(fmt == 'O' || fmt == 'R' || fmt == 'C');
+    RBH_REQUIRE(n_rows >= 0 && n_cols >= 0 && nnz >= 0);
+    if (nnz == 0) return RBH_OK;
+    RBH_REQUIRE(A_p != nullptr && A_i != nullptr && A_v != nullptr);
+    const int64_t np = fmt == 'O' ? nnz : (fmt == 'R' ? n_rows + 1 : n_cols + 1);
+    void *dp, *di, *dv;
+    RBH_HIP(st.map(A_p, sizeof(int64_t) * np, true, false, &dp));
+    RBH_HIP(st.map(A_i, sizeof(int64_t) * nnz, true, false, &di));
+    RBH_HIP(st.map(A_v, sizeof(T) * nnz, true, false, &dv));
+    *vals = (const T *)dv;
+    if (fmt == 'O') {
+        *rows = (const int64_t *)dp;
+        *cols = (const int64_t *)di;
+        return RBH_OK;
+    }
+    RBH_HIP(hipMallocAsync(ws, sizeof(int64_t) * nnz, s));
+    int64_t *major = (int64_t *)*ws;
+    RBH_HIP(launch_expand_ptr(fmt == 'R' ? n_rows : n_cols, (const int64_t *)dp, major, s));
+    *rows = fmt == 'R' ? major : (const int64_t *)di;
+    *cols = fmt == 'R' ? (const int64_t *)di : major;
+    return RBH_OK;
+}
+
+// submat(S) (rs x cs at (ro_s, co_s)) as a strided device matrix: element (r, c) at ptr[r sr + c sc].
+// S.buff when given (its layout); otherwise a ColMajor device fill of the window, as fill_dense.
+template <typename T>
+int submat_dense(Stager &st, const rbh_dense_dist *D, const rbh_state *seed, const T *S_buff, char S_layout,
+                 int64_t rs, int64_t cs, int64_t ro_s, int64_t co_s, const T **ptr, int64_t *sr, int64_t *sc,
+                 void **ws, hipStream_t s) {
+    *ws = nullptr;
+    if (S_buff) {
+        RBH_REQUIRE(S_layout == 'C' || S_layout == 'R');
+        void *dS;
+        RBH_HIP(st.map(S_buff, sizeof(T) * D->n_rows * D->n_cols, true, false, &dS));
+        *sr = S_layout == 'C' ? 1 : D->n_cols;
+        *sc = S_layout == 'C' ? D->n_rows : 1;
+        *ptr = (const T *)dS + ro_s * *sr + co_s * *sc;
+        return RBH_OK;
+    }
+    RBH_REQUIRE(seed != nullptr);
+    RBH_REQUIRE(D->family != 'B');
+    RBH_REQUIRE(D->major_axis != 'U');
+    RBH_HIP(hipMallocAsync(ws, sizeof(T) * (size_t)std::max<int64_t>(rs * cs, 1), s));
+    const char nat = dist_to_layout(D);
+    GenOperand g{};
+    memcpy(g.ctr, seed->counter, sizeof g.ctr);
+    memcpy(g.key, seed->key, sizeof g.key);
+    g.stride = (uint64_t)((major_axis_length(D) + 3) / 4);
+    g.family = D->family == 'U' ? rb::UNIFORM : rb::GAUSSIAN;
+    g.scale = (double)(T)std::sqrt(3.0);
+    int64_t n_rows_, n_cols_;
+    if (nat == 'C') { n_rows_ = cs; n_cols_ = rs; g.pr0 = co_s; g.pc0 = ro_s; }
+    else { n_rows_ = rs; n_cols_ = cs; g.pr0 = ro_s; g.pc0 = co_s; }
+    if (rs > 0 && cs > 0) RBH_HIP(launch_fill_t<T>(g, n_rows_, n_cols_, nat != 'C', (T *)*ws, s));
+    *ptr = (const T *)*ws;
+    *sr = 1;
+    *sc = rs;
+    return RBH_OK;
+}
+
+// left: B = alpha op(submat(S)) op(submat(A)) + beta B, A sparse     (sparse_data::lsksp3, sksp.hh:147-192)
+// right: B = alpha op(submat(A)) op(submat(S)) + beta B, A sparse    (sparse_data::rsksp3, sksp.hh:302-350)
+template <typename T>
+int sksp3(bool left, char layout, char opS, char opA, int64_t M, int64_t N, int64_t K, T alpha,
+          const rbh_dense_dist *D, const rbh_state *seed, const T *S_buff, char S_layout, int64_t ro_s, int64_t co_s,
+          char A_fmt, int64_t A_rows, int64_t A_cols, int64_t A_nnz, const int64_t *A_p, const int64_t *A_i,
+          const T *A_v, int64_t ro_a, int64_t co_a, T beta, T *B, int64_t ldb, void *stream) {
+    // left: (M, N, K) = (d, n, m), B d x n; right: (M, N, K) = (m, d, n), B m x d
+    RBH_REQUIRE(layout == 'C' || layout == 'R');
+    RBH_REQUIRE(opS == 'N' || opS == 'T');
+    RBH_REQUIRE(opA == 'N' || opA == 'T');
+    RBH_REQUIRE(D != nullptr);
+    RBH_REQUIRE(M >= 0 && N >= 0 && K >= 0 && ro_s >= 0 && co_s >= 0 && ro_a >= 0 && co_a >= 0);
+    // op(submat(S)) is M x K (left) or K x N (right); op(submat(A)) is K x N (left) or M x K (right)
+    const int64_t sR = left ? M : K, sC = left ? K : N, aR = left ? K : M, aC = left ? N : K;
+    const int64_t rows_submat_S = opS == 'N' ? sR : sC, cols_submat_S = opS == 'N' ? sC : sR;
+    const int64_t rows_submat_A = opA == 'N' ? aR : aC, cols_submat_A = opA == 'N' ? aC : aR;
+    RBH_REQUIRE(A_rows >= rows_submat_A + ro_a);
+    RBH_REQUIRE(A_cols >= cols_submat_A + co_a);
+    RBH_REQUIRE(D->n_rows >= rows_submat_S + ro_s);
+    RBH_REQUIRE(D->n_cols >= cols_submat_S + co_s);
+    if (layout == 'C') {
+        RBH_REQUIRE(ldb >= M);
+    } else {
+        RBH_REQUIRE(ldb >= N);
+    }
+    hipStream_t s = (hipStream_t)stream;
+    Stager st(s);
+    void *dB;
+    RBH_HIP(st.map(B, sizeof(T) * extent(layout, M, N, ldb), beta != (T)0, true, &dB));
+    const T *Sp = nullptr;
+    int64_t sr = 1, sc = 1;
+    void *sws = nullptr, *aws = nullptr;
+    int rc = submat_dense<T>(st, D, seed, S_buff, S_layout, rows_submat_S, cols_submat_S, ro_s, co_s, &Sp, &sr, &sc,
+                             &sws, s);
+    const int64_t *ar = nullptr, *ac = nullptr;
+    const T *av = nullptr;
+    if (!rc) rc = data_as_coo<T>(st, A_fmt, A_rows, A_cols, A_nnz, A_p, A_i, A_v, &ar, &ac, &av, &aws, s);
+    if (rc) {
+        if (sws) (void)hipFreeAsync(sws, s);
+        if (aws) (void)hipFreeAsync(aws, s);
+        return rc;
+    }
+    SparseApply p{};
+    p.alpha = alpha;
+    p.beta = beta;
+    p.ro = ro_a;
+    p.co = co_a;
+    p.Y = Sp;
+    p.C = dB;
+    const bool col = layout == 'C';
+    if (left) {
+        // B^T (n x d) = op(Asub)^T (n x m) op(Ssub)^T (m x d): operator (i, k) = op(Asub)(k, i)
+        p.M = N; p.N = M; p.K = K;
+        p.transposed = opA == 'N';
+        p.win_r = opA == 'N' ? K : N;
+        p.win_c = opA == 'N' ? N : K;
+        // Y(k, j) = op(Ssub)(j, k)
+        p.ysk = opS == 'N' ? sc : sr;
+        p.ysj = opS == 'N' ? sr : sc;
+        // C(i, j) = B(j, i)
+        p.crs = col ? ldb : 1;
+        p.ccs = col ? 1 : ldb;
+    } else {
+        // B (m x d) = op(Asub) (m x n) op(Ssub) (n x d): operator (i, k) = op(Asub)(i, k)
+        p.M = M; p.N = N; p.K = K;
+        p.transposed = opA == 'T';
+        p.win_r = opA == 'N' ? M : K;
+        p.win_c = opA == 'N' ? K : M;
+        // Y(k, j) = op(Ssub)(k, j)
+        p.ysk = opS == 'N' ? sr : sc;
+        p.ysj = opS == 'N' ? sc : sr;
+        p.crs = col ? 1 : ldb;
+        p.ccs = col ? ldb : 1;
+    }
+    const int64_t nnz = (alpha == (T)0) ? 0 : A_nnz;   // beta scaling only, as left_spmm (:134-135)
+    hipError_t e = run_sparse_apply_t<T>(p, ar, ac, av, nnz, s);
+    if (sws) (void)hipFreeAsync(sws, s);
+    if (aws) (void)hipFreeAsync(aws, s);
+    RBH_HIP(e);
+    RBH_HIP(st.finish());
+    return RBH_OK;
+}
+
 template <typename T> hipError_t launch_sym_t(char, const T *, int64_t, int64_t, T, int *, hipStream_t);
 template <> hipError_t launch_sym_t<double>(char l, const double *A, int64_t n, int64_t lda, double tol, int *f, hipStream_t s) {
     return launch_symcheck_f64(l, A, n, lda, tol, f, s);
@@ -741,6 +901,39 @@ int rbh_rskge3_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_
                    int64_t ro_s, int64_t co_s, float beta, float *B, int64_t ldb, void *stream) {
     return rskge3<float>(layout, opA, opS, m, d, n, alpha, A, lda, D, seed, S_buff, S_layout, ro_s, co_s, beta, B,
                          ldb, stream);
+}
+
+int rbh_lsksp3_f64(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, double alpha,
+                   const rbh_dense_dist *D, const rbh_state *seed, const double *S_buff, char S_layout, int64_t ro_s,
+                   int64_t co_s, char A_fmt, int64_t A_rows, int64_t A_cols, int64_t A_nnz, const int64_t *A_p,
+                   const int64_t *A_i, const double *A_v, int64_t ro_a, int64_t co_a, double beta, double *B,
+                   int64_t ldb, void *stream) {
+    return sksp3<double>(true, layout, opS, opA, d, n, m, alpha, D, seed, S_buff, S_layout, ro_s, co_s, A_fmt, A_rows,
+                         A_cols, A_nnz, A_p, A_i, A_v, ro_a, co_a, beta, B, ldb, stream);
+}
+int rbh_lsksp3_f32(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, float alpha,
+                   const rbh_dense_dist *D, const rbh_state *seed, const float *S_buff, char S_layout, int64_t ro_s,
+                   int64_t co_s, char A_fmt, int64_t A_rows, int64_t A_cols, int64_t A_nnz, const int64_t *A_p,
+                   const int64_t *A_i, const float *A_v, int64_t ro_a, int64_t co_a, float beta, float *B,
+                   int64_t ldb, void *stream) {
+    return sksp3<float>(true, layout, opS, opA, d, n, m, alpha, D, seed, S_buff, S_layout, ro_s, co_s, A_fmt, A_rows,
+                        A_cols, A_nnz, A_p, A_i, A_v, ro_a, co_a, beta, B, ldb, stream);
+}
+int rbh_rsksp3_f64(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, double alpha, char A_fmt,
+                   int64_t A_rows, int64_t A_cols, int64_t A_nnz, const int64_t *A_p, const int64_t *A_i,
+                   const double *A_v, int64_t ro_a, int64_t co_a, const rbh_dense_dist *D, const rbh_state *seed,
+                   const double *S_buff, char S_layout, int64_t ro_s, int64_t co_s, double beta, double *B,
+                   int64_t ldb, void *stream) {
+    return sksp3<double>(false, layout, opS, opA, m, d, n, alpha, D, seed, S_buff, S_layout, ro_s, co_s, A_fmt, A_rows,
+                         A_cols, A_nnz, A_p, A_i, A_v, ro_a, co_a, beta, B, ldb, stream);
+}
+int rbh_rsksp3_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, float alpha, char A_fmt,
+                   int64_t A_rows, int64_t A_cols, int64_t A_nnz, const int64_t *A_p, const int64_t *A_i,
+                   const float *A_v, int64_t ro_a, int64_t co_a, const rbh_dense_dist *D, const rbh_state *seed,
+                   const float *S_buff, char S_layout, int64_t ro_s, int64_t co_s, float beta, float *B, int64_t ldb,
+                   void *stream) {
+    return sksp3<float>(false, layout, opS, opA, m, d, n, alpha, D, seed, S_buff, S_layout, ro_s, co_s, A_fmt, A_rows,
+                        A_cols, A_nnz, A_p, A_i, A_v, ro_a, co_a, beta, B, ldb, stream);
 }
 
 int rbh_lskges_f64(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, double alpha,

@@ -1015,6 +1015,22 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     su_epilogue<T>(acc, reinterpret_cast<T *>(smem), p, row0, j0, wave, lane, vec_out);
 }
 
+// ------------------------------------------------------------------------------------------
+// 6. CSR / CSC pointer arrays -> per-entry major indices (sketch_sparse's data matrix as COO):
+//    out[e] = r for rowptr[r] <= e < rowptr[r + 1]. One thread per major index.
+// ------------------------------------------------------------------------------------------
+__global__ void expand_ptr_kernel(int64_t n_major, const int64_t *ptr, int64_t *out) {
+    const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (r >= n_major) return;
+    for (int64_t e = ptr[r]; e < ptr[r + 1]; ++e) out[e] = r;
+}
+
+hipError_t launch_expand_ptr(int64_t n_major, const int64_t *ptr, int64_t *out, hipStream_t s) {
+    if (n_major <= 0) return hipSuccess;
+    hipLaunchKernelGGL(expand_ptr_kernel, dim3((unsigned)((n_major + 255) / 256)), dim3(256), 0, s, n_major, ptr, out);
+    return hipGetLastError();
+}
+
 template <typename T>
 static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, const int64_t *cols, const T *vals,
                                      int64_t nnz, hipStream_t s) {

@@ -36,6 +36,9 @@ hipError_t run_sparse_apply_f64(const SparseApply &p, const int64_t *rows, const
 hipError_t run_sparse_apply_f32(const SparseApply &p, const int64_t *rows, const int64_t *cols, const float *vals,
                                 int64_t nnz, hipStream_t s);
 
+// CSR/CSC pointer array (n_major + 1 entries) -> the major index of every entry (saso.hip).
+hipError_t launch_expand_ptr(int64_t n_major, const int64_t *ptr, int64_t *out, hipStream_t s);
+
 // util::require_symmetric on the device (sksy.hip). Writes 0/1 (violation found) to *flag.
 hipError_t launch_symcheck_f64(char layout, const double *A, int64_t n, int64_t lda, double tol, int *flag,
                                hipStream_t s);
