@@ -6,7 +6,9 @@
 //   DenseDistName / DenseDist / DenseSkOp (dense_skops.hh:204-419), fill_dense x3 (:486-592),
 //   SparseDist / SparseSkOp / fill_sparse (sparse_skops.hh:134-413),
 //   sketch_general x8 (skge.hh:771-1214), sketch_symmetric x4 (sksy.hh:165-537),
-//   sketch_vector x2 (skve.hh:152-258),
+//   sketch_vector x2 (skve.hh:152-258), sparse_data::{COO,CSR,CSC}Matrix views
+//   (sparse_data/{coo,csr,csc}_matrix.hh, int64 zero-based indices) and sketch_sparse x2
+//   (sparse_data/sksp.hh:464-615),
 //   exceptions::Error (exceptions.hh:45-70), and the blas::Layout / blas::Op enums of BLAS++,
 // and routes every call to the MI355X C ABI (include/randblas_hip.h). Host arrays work as in
 // the reference (they are staged through HBM; the call is synchronous); device arrays
@@ -233,6 +235,8 @@ template <> struct Api<double> {
     static constexpr auto lskges = rbh_lskges_f64;
     static constexpr auto rskges = rbh_rskges_f64;
     static constexpr auto sym = rbh_require_symmetric_f64;
+    static constexpr auto lsksp3 = rbh_lsksp3_f64;
+    static constexpr auto rsksp3 = rbh_rsksp3_f64;
 };
 template <> struct Api<float> {
     static int fill_dense(char l, const rbh_dense_dist *D, int64_t r, int64_t c, int64_t ro, int64_t co, float *b,
@@ -245,6 +249,8 @@ template <> struct Api<float> {
     static constexpr auto lskges = rbh_lskges_f32;
     static constexpr auto rskges = rbh_rskges_f32;
     static constexpr auto sym = rbh_require_symmetric_f32;
+    static constexpr auto lsksp3 = rbh_lsksp3_f32;
+    static constexpr auto rsksp3 = rbh_rsksp3_f32;
 };
 }  // namespace detail
 
@@ -515,6 +521,121 @@ inline void sketch_vector(blas::Op opS, int64_t d, int64_t m, T alpha, SKOP &S, 
 template <typename T, typename SKOP>
 inline void sketch_vector(blas::Op opS, T alpha, SKOP &S, const T *x, int64_t incx, T beta, T *y, int64_t incy) {
     sketch_vector(opS, S.dist.n_rows, S.dist.n_cols, alpha, S, (int64_t)0, (int64_t)0, x, incx, beta, y, incy);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Sparse data matrices (sparse_data/{coo,csr,csc}_matrix.hh) and sketch_sparse (sparse_data/sksp.hh)
+// ---------------------------------------------------------------------------------------------
+namespace sparse_data {
+enum class IndexBase : char { Zero = 'Z', One = 'O' };   // sparse_data/base.hh:39-48
+
+// Views over caller arrays (host or device), the reference's non-owning constructors; the owning
+// (n_rows, n_cols) constructor + reserve(nnz) allocates host arrays, as the reference does.
+template <typename T, typename sint_t = int64_t>
+struct COOMatrix {
+    static_assert(sizeof(sint_t) == 8, "librandblas_hip takes int64 indices");
+    const int64_t n_rows, n_cols;
+    const bool own_memory;
+    int64_t nnz = 0;
+    IndexBase index_base = IndexBase::Zero;
+    T *vals = nullptr;
+    sint_t *rows = nullptr, *cols = nullptr;
+    COOMatrix(int64_t n_rows, int64_t n_cols, int64_t nnz, T *vals, sint_t *rows, sint_t *cols,
+              bool compute_sort_type = true, IndexBase index_base = IndexBase::Zero)
+        : n_rows(n_rows), n_cols(n_cols), own_memory(false), nnz(nnz), index_base(index_base), vals(vals), rows(rows),
+          cols(cols) { (void)compute_sort_type; }
+    COOMatrix(int64_t n_rows, int64_t n_cols) : n_rows(n_rows), n_cols(n_cols), own_memory(true) {}
+    void reserve(int64_t n) {
+        RBH_CXX_REQUIRE(own_memory && vals == nullptr);
+        nnz = n; vals = new T[n]; rows = new sint_t[n]; cols = new sint_t[n];
+    }
+    ~COOMatrix() { if (own_memory) { delete[] vals; delete[] rows; delete[] cols; } }
+    COOMatrix(const COOMatrix &) = delete;
+    static constexpr char fmt = 'O';
+    const sint_t *ptr_arr() const { return rows; }
+    const sint_t *idx_arr() const { return cols; }
+};
+
+template <typename T, typename sint_t = int64_t>
+struct CSRMatrix {
+    static_assert(sizeof(sint_t) == 8, "librandblas_hip takes int64 indices");
+    const int64_t n_rows, n_cols;
+    const bool own_memory;
+    int64_t nnz = 0;
+    IndexBase index_base = IndexBase::Zero;
+    T *vals = nullptr;
+    sint_t *rowptr = nullptr, *colidxs = nullptr;
+    CSRMatrix(int64_t n_rows, int64_t n_cols, int64_t nnz, T *vals, sint_t *rowptr, sint_t *colidxs,
+              IndexBase index_base = IndexBase::Zero)
+        : n_rows(n_rows), n_cols(n_cols), own_memory(false), nnz(nnz), index_base(index_base), vals(vals),
+          rowptr(rowptr), colidxs(colidxs) {}
+    CSRMatrix(int64_t n_rows, int64_t n_cols) : n_rows(n_rows), n_cols(n_cols), own_memory(true) {}
+    void reserve(int64_t n) {
+        RBH_CXX_REQUIRE(own_memory && vals == nullptr);
+        nnz = n; vals = new T[n]; rowptr = new sint_t[n_rows + 1]; colidxs = new sint_t[n];
+    }
+    ~CSRMatrix() { if (own_memory) { delete[] vals; delete[] rowptr; delete[] colidxs; } }
+    CSRMatrix(const CSRMatrix &) = delete;
+    static constexpr char fmt = 'R';
+    const sint_t *ptr_arr() const { return rowptr; }
+    const sint_t *idx_arr() const { return colidxs; }
+};
+
+template <typename T, typename sint_t = int64_t>
+struct CSCMatrix {
+    static_assert(sizeof(sint_t) == 8, "librandblas_hip takes int64 indices");
+    const int64_t n_rows, n_cols;
+    const bool own_memory;
+    int64_t nnz = 0;
+    IndexBase index_base = IndexBase::Zero;
+    T *vals = nullptr;
+    sint_t *colptr = nullptr, *rowidxs = nullptr;
+    CSCMatrix(int64_t n_rows, int64_t n_cols, int64_t nnz, T *vals, sint_t *rowidxs, sint_t *colptr,
+              IndexBase index_base = IndexBase::Zero)
+        : n_rows(n_rows), n_cols(n_cols), own_memory(false), nnz(nnz), index_base(index_base), vals(vals),
+          colptr(colptr), rowidxs(rowidxs) {}
+    CSCMatrix(int64_t n_rows, int64_t n_cols) : n_rows(n_rows), n_cols(n_cols), own_memory(true) {}
+    void reserve(int64_t n) {
+        RBH_CXX_REQUIRE(own_memory && vals == nullptr);
+        nnz = n; vals = new T[n]; colptr = new sint_t[n_cols + 1]; rowidxs = new sint_t[n];
+    }
+    ~CSCMatrix() { if (own_memory) { delete[] vals; delete[] colptr; delete[] rowidxs; } }
+    CSCMatrix(const CSCMatrix &) = delete;
+    static constexpr char fmt = 'C';
+    const sint_t *ptr_arr() const { return colptr; }
+    const sint_t *idx_arr() const { return rowidxs; }
+};
+}  // namespace sparse_data
+using sparse_data::COOMatrix;
+using sparse_data::CSCMatrix;
+using sparse_data::CSRMatrix;
+
+// B = alpha op(submat(S)) op(submat(A)) + beta B, A sparse (sksp.hh:464-485 -> lsksp3, :147-192)
+template <typename T, typename SpMat, typename RNG>
+inline void sketch_sparse(blas::Layout layout, blas::Op opS, blas::Op opA, int64_t d, int64_t n, int64_t m, T alpha,
+                          DenseSkOp<T, RNG> &S, int64_t ro_s, int64_t co_s, SpMat &A, int64_t ro_a, int64_t co_a,
+                          T beta, T *B, int64_t ldb) {
+    RBH_CXX_REQUIRE(A.index_base == sparse_data::IndexBase::Zero);
+    const rbh_dense_dist dd = c_dist(S.dist);
+    const rbh_state s = detail::c_state(S.seed_state);
+    detail::check(detail::Api<T>::lsksp3((char)layout, (char)opS, (char)opA, d, n, m, alpha, &dd, &s, S.buff,
+                                         (char)S.layout, ro_s, co_s, SpMat::fmt, A.n_rows, A.n_cols, A.nnz,
+                                         (const int64_t *)A.ptr_arr(), (const int64_t *)A.idx_arr(), A.vals, ro_a,
+                                         co_a, beta, B, ldb, nullptr));
+}
+
+// B = alpha op(submat(A)) op(submat(S)) + beta B, A sparse (sksp.hh:595-615 -> rsksp3, :302-350)
+template <typename T, typename SpMat, typename RNG>
+inline void sketch_sparse(blas::Layout layout, blas::Op opA, blas::Op opS, int64_t m, int64_t d, int64_t n, T alpha,
+                          SpMat &A, int64_t ro_a, int64_t co_a, DenseSkOp<T, RNG> &S, int64_t ro_s, int64_t co_s,
+                          T beta, T *B, int64_t ldb) {
+    RBH_CXX_REQUIRE(A.index_base == sparse_data::IndexBase::Zero);
+    const rbh_dense_dist dd = c_dist(S.dist);
+    const rbh_state s = detail::c_state(S.seed_state);
+    detail::check(detail::Api<T>::rsksp3((char)layout, (char)opA, (char)opS, m, d, n, alpha, SpMat::fmt, A.n_rows,
+                                         A.n_cols, A.nnz, (const int64_t *)A.ptr_arr(), (const int64_t *)A.idx_arr(),
+                                         A.vals, ro_a, co_a, &dd, &s, S.buff, (char)S.layout, ro_s, co_s, beta, B,
+                                         ldb, nullptr));
 }
 
 }  // namespace RandBLAS

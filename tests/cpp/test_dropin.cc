@@ -200,6 +200,59 @@ static void vector_sketch() {
     }
 }
 
+static void sparse_data_sketch() {
+    // sketch_sparse (sksp.hh:464-615): CSR data on the left sketch, COO data on the right sketch
+    const int64_t m = 50, n = 40, d = 8;
+    std::vector<double> Ad(m * n, 0.0);   // dense image, ColMajor
+    std::vector<int64_t> rowptr(m + 1, 0), colidx, crow, ccol;
+    std::vector<double> vals;
+    for (int64_t i = 0; i < m; ++i) {
+        for (int64_t j = 0; j < n; ++j)
+            if ((i * 7 + j * 3) % 11 == 0) {
+                const double v = 0.25 * (double)((i + 2 * j) % 9) - 1.0;
+                colidx.push_back(j); crow.push_back(i); ccol.push_back(j); vals.push_back(v);
+                Ad[i + j * m] = v;
+            }
+        rowptr[i + 1] = (int64_t)colidx.size();
+    }
+    const int64_t nnz = (int64_t)vals.size();
+    RandBLAS::CSRMatrix<double> Acsr(m, n, nnz, vals.data(), rowptr.data(), colidx.data());
+    RandBLAS::COOMatrix<double> Acoo(m, n, nnz, vals.data(), crow.data(), ccol.data());
+    const double eps = std::numeric_limits<double>::epsilon();
+    // left: B (d x n) = S (d x m) A
+    RandBLAS::DenseDist DL(d, m);
+    RandBLAS::DenseSkOp<double> SL(DL, 5);
+    std::vector<double> BL(d * n, 0.0), SeL(d * m);
+    RandBLAS::sketch_sparse(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, m, 1.0, SL, 0, 0, Acsr, 0, 0, 0.0,
+                            BL.data(), d);
+    RandBLAS::fill_dense(Layout::ColMajor, DL, d, m, 0, 0, SeL.data(), SL.seed_state);
+    for (int64_t i = 0; i < d; ++i)
+        for (int64_t j = 0; j < n; ++j) {
+            double ex = 0, bound = 0;
+            for (int64_t k = 0; k < m; ++k) {
+                ex += SeL[i + k * d] * Ad[k + j * m];
+                bound += std::fabs(SeL[i + k * d] * Ad[k + j * m]);
+            }
+            CHECK(std::fabs(BL[i + j * d] - ex) <= bound * m * 2 * eps + 1e-300);
+        }
+    // right: B (m x d) = A (m x n) S (n x d)
+    RandBLAS::DenseDist DR(n, d);
+    RandBLAS::DenseSkOp<double> SR(DR, 6);
+    std::vector<double> BR(m * d, 0.0), SeR(n * d);
+    RandBLAS::sketch_sparse(Layout::ColMajor, Op::NoTrans, Op::NoTrans, m, d, n, 1.0, Acoo, 0, 0, SR, 0, 0, 0.0,
+                            BR.data(), m);
+    RandBLAS::fill_dense(Layout::ColMajor, DR, n, d, 0, 0, SeR.data(), SR.seed_state);
+    for (int64_t i = 0; i < m; ++i)
+        for (int64_t j = 0; j < d; ++j) {
+            double ex = 0, bound = 0;
+            for (int64_t k = 0; k < n; ++k) {
+                ex += Ad[i + k * m] * SeR[k + j * n];
+                bound += std::fabs(Ad[i + k * m] * SeR[k + j * n]);
+            }
+            CHECK(std::fabs(BR[i + j * m] - ex) <= bound * n * 2 * eps + 1e-300);
+        }
+}
+
 int main() {
     dense_left<double>(Layout::ColMajor);
     dense_left<double>(Layout::RowMajor);
@@ -208,6 +261,7 @@ int main() {
     sparse_left();
     symmetric_and_errors();
     vector_sketch();
+    sparse_data_sketch();
     if (g_fail) {
         std::printf("%d checks FAILED\n", g_fail);
         return 1;
