@@ -832,6 +832,35 @@ struct SdAcc {
     }
 };
 
+#ifndef SD_NO_BATCH
+#define SD_BATCH 1
+#endif
+#ifdef SD_BATCH
+// four entries in one index-mode section: the row index moves with s_set_gpr_idx_idx, so the mode
+// is toggled once per four adds (the sign flips are done before the section)
+__device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t (&w)[4], const double (&y)[4]) {
+    double ys[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint32_t m;
+        asm("s_and_b32 %0, %1, 0x80000000" : "=s"(m) : "s"(w[q]) : "scc");
+        ys[q] = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, y[q]) ^ ((uint64_t)m << 32));
+    }
+    asm volatile("s_set_gpr_idx_on %3, gpr_idx(SRC0,DST)\n\t"
+                 "v_add_f64 v[32:33], v[32:33], %7\n\t"
+                 "s_set_gpr_idx_idx %4\n\t"
+                 "v_add_f64 v[32:33], v[32:33], %8\n\t"
+                 "s_set_gpr_idx_idx %5\n\t"
+                 "v_add_f64 v[32:33], v[32:33], %9\n\t"
+                 "s_set_gpr_idx_idx %6\n\t"
+                 "v_add_f64 v[32:33], v[32:33], %10\n\t"
+                 "s_set_gpr_idx_off"
+                 : "+{v[32:63]}"(acc.a), "+{v[64:95]}"(acc.b), "+{v[96:97]}"(acc.dmy)
+                 : "s"(w[0]), "s"(w[1]), "s"(w[2]), "s"(w[3]), "v"(ys[0]), "v"(ys[1]), "v"(ys[2]), "v"(ys[3])
+                 : "m0", "scc");
+}
+#endif
+
 __device__ __forceinline__ uint32_t lds_addr(const void *ptr) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)ptr;
 }
@@ -979,8 +1008,13 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
                 }
             };
             auto update = [&](const T (&y)[SU_D], const uint32_t (&w)[SU_D]) {
+#ifdef SD_BATCH
+                static_assert(SU_D == 4, "batched update takes four entries");
+                sd_add4(acc, w, y);
+#else
 #pragma unroll
                 for (int q = 0; q < SU_D; ++q) acc.add_at(w[q], y[q]);
+#endif
             };
             T ya[SU_D], yb[SU_D];
             uint32_t wa[SU_D], wb[SU_D];
