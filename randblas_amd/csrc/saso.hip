@@ -26,6 +26,7 @@
 #include "common.hpp"
 #include "saso.hpp"
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 namespace rbh {
 
@@ -1065,11 +1066,117 @@ hipError_t launch_expand_ptr(int64_t n_major, const int64_t *ptr, int64_t *out, 
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------
+// 7. CSR build without a sort, for operators whose (row, k) entries are distinct (every sampled
+//    SASO / LASO): bit (k % SP_KC) of mask[v] marks an entry of virtual row v; the entry's CSR
+//    position is the row's start plus the number of marked bits below it, i.e. its rank in
+//    ascending k -- the order the sort produces.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool sp_locate(int64_t e, const int64_t *rows, const int64_t *cols, const SparseApply &p,
+                                          int64_t &v, uint32_t &kk, int64_t &i) {
+    const int64_t wr = rows[e] - p.ro, wc = cols[e] - p.co;
+    if (!(wr >= 0 && wr < p.win_r && wc >= 0 && wc < p.win_c)) return false;
+    i = p.transposed ? wc : wr;
+    const int64_t k = p.transposed ? wr : wc;
+    v = (k / SP_KC) * p.M + i;
+    kk = (uint32_t)(k % SP_KC);
+    return true;
+}
+
+__global__ void mark_kernel(int64_t nnz, const int64_t *rows, const int64_t *cols, const SparseApply p,
+                            uint32_t *mask) {
+    const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    int64_t v, i;
+    uint32_t kk;
+    if (e < nnz && sp_locate(e, rows, cols, p, v, kk, i)) atomicOr(&mask[v * 4 + kk / 32], 1u << (kk % 32));
+}
+
+__global__ void mask_count_kernel(int64_t NV, const uint32_t *mask, int32_t *cnt) {
+    const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (v > NV) return;
+    cnt[v] = v < NV ? __popc(mask[4 * v]) + __popc(mask[4 * v + 1]) + __popc(mask[4 * v + 2]) + __popc(mask[4 * v + 3])
+                    : 0;
+}
+
+template <typename T>
+__global__ void place_kernel(int64_t nnz, const int64_t *rows, const int64_t *cols, const T *vals, const SparseApply p,
+                             const uint32_t *mask, const int32_t *vrp, uint32_t *rec, uint32_t kmul) {
+    const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    int64_t v, i;
+    uint32_t kk;
+    if (e >= nnz || !sp_locate(e, rows, cols, p, v, kk, i)) return;
+    const uint32_t *mw = mask + 4 * v;
+    uint32_t rank = __popc(mw[kk / 32] & ((1u << (kk % 32)) - 1u));
+    for (uint32_t w = 0; w < kk / 32; ++w) rank += __popc(mw[w]);
+    const uint32_t row = (uint32_t)(i % 32);
+    const T x = (T)p.alpha * vals[e];
+    rec[vrp[v] + rank] = (sizeof(T) == 8 ? 2u * row : row) | ((kk * kmul) << 8) | (signbit(x) ? 0x80000000u : 0u);
+}
+
+// The LDS-DMA apply (section 5) on a sort-free CSR.
+static hipError_t run_sparse_dma(const SparseApply &p, const int64_t *rows, const int64_t *cols, const double *vals,
+                                 int64_t nnz, bool y_k, hipStream_t s) {
+    const int64_t nchunks = p.K > 0 ? (p.K + SP_KC - 1) / SP_KC : 0;
+    const int64_t NV = nchunks * p.M;
+    const size_t n = (size_t)(nnz > 0 ? nnz : 1);
+    size_t scan_bytes = 0;
+    hipError_t err = rocprim::exclusive_scan(nullptr, scan_bytes, (const int32_t *)nullptr, (int32_t *)nullptr, 0,
+                                             (size_t)(NV + 1), rocprim::plus<int32_t>(), s);
+    if (err != hipSuccess) return err;
+    const size_t bytes = (size_t)NV * 16 + 2 * (size_t)(NV + 1) * sizeof(int32_t) + n * sizeof(uint32_t) + scan_bytes + 256;
+    char *ws = nullptr;
+    err = hipMallocAsync((void **)&ws, bytes, s);
+    if (err != hipSuccess) return err;
+    size_t off = 0;
+    auto carve = [&](size_t b) { void *q = ws + off; off += (b + 15) & ~(size_t)15; return q; };
+    uint32_t *mask = (uint32_t *)carve((size_t)NV * 16);
+    int32_t *cnt = (int32_t *)carve((size_t)(NV + 1) * sizeof(int32_t));
+    int32_t *vrp = (int32_t *)carve((size_t)(NV + 1) * sizeof(int32_t));
+    uint32_t *rec = (uint32_t *)carve(n * sizeof(uint32_t));
+    void *tmp = carve(scan_bytes);
+    const uint32_t kmul = y_k ? (uint32_t)sizeof(double) : (uint32_t)(SU_J * sizeof(double));
+    err = hipMemsetAsync(mask, 0, (size_t)NV * 16, s);
+    if (err == hipSuccess && nnz > 0) {
+        hipLaunchKernelGGL(mark_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, rows, cols, p, mask);
+        err = hipGetLastError();
+    }
+    if (err == hipSuccess) {
+        hipLaunchKernelGGL(mask_count_kernel, dim3((unsigned)((NV + 1 + 255) / 256)), dim3(256), 0, s, NV, mask, cnt);
+        err = rocprim::exclusive_scan(tmp, scan_bytes, cnt, vrp, 0, (size_t)(NV + 1), rocprim::plus<int32_t>(), s);
+    }
+    if (err == hipSuccess && nnz > 0) {
+        hipLaunchKernelGGL(place_kernel<double>, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, rows, cols,
+                           vals, p, mask, vrp, rec, kmul);
+        err = hipGetLastError();
+    }
+    if (err == hipSuccess) {
+        timing_begin(s);
+        const int64_t nrb_u = (p.M + SU_ROWS - 1) / SU_ROWS;
+        const dim3 grid_u((unsigned)(((p.N + SU_J - 1) / SU_J) * nrb_u));
+        const int vec_out = p.crs == 1 && (p.ccs % 2) == 0 && (((uintptr_t)p.C) % 16) == 0;
+        if (y_k) hipLaunchKernelGGL((saso_dma_kernel<false>), grid_u, dim3(SU_NT), 0, s, p, vrp, rec, nchunks, nrb_u, vec_out);
+        else hipLaunchKernelGGL((saso_dma_kernel<true>), grid_u, dim3(SU_NT), 0, s, p, vrp, rec, nchunks, nrb_u, vec_out);
+        err = hipGetLastError();
+        timing_end(s);
+    }
+    hipError_t e2 = hipFreeAsync(ws, s);
+    return err != hipSuccess ? err : e2;
+}
+
 template <typename T>
 static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, const int64_t *cols, const T *vals,
                                      int64_t nnz, hipStream_t s) {
     if (p.M <= 0 || p.N <= 0) return hipSuccess;
     if (nnz >= (int64_t)0x7fffffff) return hipErrorInvalidValue;
+    {   // LDS-DMA kernel (section 5) on the sort-free CSR (section 7): f64, values +-1 (operator
+        // sampled in this call: distinct entries), |alpha| = 1
+        constexpr int VEC = SuCfg<T>::VEC;
+        static const bool dma_off = [] { const char *e = getenv("RBH_NO_SASO_DMA"); return e && e[0] == '1'; }();
+        const bool y_k = p.ysk == 1 && (p.ysj % VEC) == 0 && (((uintptr_t)p.Y) % 16) == 0 && (p.K % VEC) == 0;
+        const bool y_jd = p.ysj == 1 && (p.ysk % VEC) == 0 && (((uintptr_t)p.Y) % 16) == 0 && (p.N % VEC) == 0;
+        if (sizeof(T) == 8 && p.unit_vals && (p.alpha == 1.0 || p.alpha == -1.0) && (y_k || y_jd) && !dma_off)
+            return run_sparse_dma(p, rows, cols, (const double *)vals, nnz, y_k, s);
+    }
     hipError_t err;
     const int64_t nchunks = p.K > 0 ? (p.K + SP_KC - 1) / SP_KC : 0;
     const int64_t NV = nchunks * p.M;
@@ -1113,37 +1220,21 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
     // f64 only: the f32 instantiation (index-mode v_add_f32) still loses entries on gfx950 with
     // nothing in flight, cause not found; f32 takes the general-value kernel
     const bool unit = (y_j || y_k) && !unit_off && sizeof(T) == 8;
-    // LDS-DMA kernel (section 5): f64, values +-1 (operator sampled in this call), |alpha| = 1
-    static const bool dma_off = [] { const char *e = getenv("RBH_NO_SASO_DMA"); return e && e[0] == '1'; }();
-    const bool y_jd = p.ysj == 1 && (p.ysk % VEC) == 0 && (((uintptr_t)p.Y) % 16) == 0 && (p.N % VEC) == 0;
-    const bool dma = sizeof(T) == 8 && p.unit_vals && (p.alpha == 1.0 || p.alpha == -1.0) && (y_k || y_jd) &&
-                     !dma_off;
-    const uint32_t kmul = (dma && !y_k) ? (uint32_t)(SU_J * sizeof(T)) : (uint32_t)sizeof(T);
+
     err = hipMemsetAsync(ut, 0, sizeof(UniformTest<T>), s);
     if (err != hipSuccess) { (void)hipFreeAsync(ws, s); return err; }
 
     if (nnz > 0) {
         hipLaunchKernelGGL(coo_keys_kernel<T>, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, rows, cols,
                            vals, p.ro, p.co, p.win_r, p.win_c, p.transposed, p.M, (T)p.alpha, k_in, v_in,
-                           (unit && !dma) ? ut : nullptr);
+                           unit ? ut : nullptr);
         // invalid keys (~0) still sort last: their low end_bit bits are all ones, above every valid key
         err = rocprim::radix_sort_pairs(tmp, tmp_bytes, k_in, k_out, v_in, v_out, (size_t)nnz, 0, (unsigned)end_bit, s);
         if (err != hipSuccess) { (void)hipFreeAsync(ws, s); return err; }
     }
     hipLaunchKernelGGL(rowptr_kernel<T>, dim3((unsigned)((nnz + 1 + 255) / 256)), dim3(256), 0, s, nnz, k_out, v_out,
-                       NV, p.M, vrp, kl, rec, kmul);
+                       NV, p.M, vrp, kl, rec, (uint32_t)sizeof(T));
     timing_begin(s);
-    if (dma) {
-        const int64_t nrb_u = (p.M + SU_ROWS - 1) / SU_ROWS;
-        const dim3 grid_u((unsigned)(((p.N + SU_J - 1) / SU_J) * nrb_u));
-        const int vec_out = p.crs == 1 && (p.ccs % VEC) == 0 && (((uintptr_t)p.C) % 16) == 0;
-        if (y_k) hipLaunchKernelGGL((saso_dma_kernel<false>), grid_u, dim3(SU_NT), 0, s, p, vrp, rec, nchunks, nrb_u, vec_out);
-        else hipLaunchKernelGGL((saso_dma_kernel<true>), grid_u, dim3(SU_NT), 0, s, p, vrp, rec, nchunks, nrb_u, vec_out);
-        err = hipGetLastError();
-        timing_end(s);
-        hipError_t e2 = hipFreeAsync(ws, s);
-        return err != hipSuccess ? err : e2;
-    }
     if (unit) {
         const int64_t nrb_u = (p.M + SU_ROWS - 1) / SU_ROWS;
         const dim3 grid_u((unsigned)(((p.N + SU_J - 1) / SU_J) * nrb_u));
