@@ -47,6 +47,8 @@ struct GemmProblem {
     int xmode, ymode;    // MEM load mode: 2 = 16-B loads along k, 1 = scalar along k, 0 = scalar along o
     MemOperand xm, ym;
     GenOperand xg, yg;
+    int splitk;          // > 1: the fused kernel splits K; workgroup z writes alpha * its partial sum
+    void *partial;       //      to partial[z] (M x N col-major), and a reduction forms C
 };
 
 // Kernel launchers (skge_dense.hip)

@@ -423,10 +423,12 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void skge_fused_kernel(cons
     if (tid < 16) tab[tid] = rb::LOGF_TAB[tid];
 
     const int64_t nTm = (p.M + BM - 1) / BM, nTn = (p.N + BN - 1) / BN;
-    const int64_t nb = nTm * nTn;
+    const int split = p.splitk > 1 ? p.splitk : 1;
+    const int64_t nb = nTm * nTn * split;
     const int64_t b = blockIdx.x;
     const int64_t xcd = b % 8, qq = nb / 8, rr = nb % 8;
-    const int64_t t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + b / 8;
+    const int64_t t_all = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + b / 8;
+    const int64_t z = t_all % split, t = t_all / split;   // the K splits of a tile run side by side
     const int64_t tm = t % nTm, tn = t / nTm;
     const int64_t i0 = tm * BM, j0 = tn * BN;
 
@@ -444,10 +446,12 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void skge_fused_kernel(cons
 #pragma unroll
         for (int c = 0; c < FB; ++c) acc[a][c] = (acc_t){0, 0, 0, 0};
 
-    const int64_t nk = (p.K + BK - 1) / BK;
+    const int64_t nk_all = (p.K + BK - 1) / BK;
+    const int64_t per = (nk_all + split - 1) / split;
+    const int64_t kt0 = z * per, kt1 = kt0 + per < nk_all ? kt0 + per : nk_all;
     __syncthreads();   // tab
-    mt.load_fast(mo, mo0, 0, mnO, p.K, tid);
-    gt.template gen<FAMILY>(go, go0, 0, gnO, p.K, tid, tab);
+    mt.load_fast(mo, mo0, kt0 * BK, mnO, p.K, tid);
+    gt.template gen<FAMILY>(go, go0, kt0 * BK, gnO, p.K, tid, tab);
     mt.template store_fast<LDK>(lds + moff, tid);
     gt.template store<LDK>(lds + goff, tid);
     __syncthreads();
@@ -462,8 +466,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void skge_fused_kernel(cons
     // one phase order per loop.)
     auto k_loop = [&](auto mfma_first_tag) {
         constexpr bool MFMA_FIRST = decltype(mfma_first_tag)::value;
-        for (int64_t kt = 0; kt < nk; ++kt) {
-            const int cur = (int)(kt & 1);
+        for (int64_t kt = kt0; kt < kt1; ++kt) {
+            const int cur = (int)((kt - kt0) & 1);
             const T *Xc = lds + cur * (XS + YS);
             const T *Yc = Xc + XS;
             T *nxt = lds + (cur ^ 1) * (XS + YS);
@@ -492,8 +496,9 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void skge_fused_kernel(cons
     if (((__builtin_amdgcn_readfirstlane(wave) >> 2) & 1) == 0) k_loop(std::true_type{});
     else k_loop(std::false_type{});
 
-    T *C = (T *)p.C;
-    const T alpha = (T)p.alpha, beta = (T)p.beta;
+    T *C = split > 1 ? (T *)p.partial + z * p.M * p.N : (T *)p.C;
+    const int64_t ldc = split > 1 ? p.M : p.ldc;
+    const T alpha = (T)p.alpha, beta = split > 1 ? (T)0 : (T)p.beta;
 #pragma unroll
     for (int a = 0; a < FA; ++a) {
         const int64_t i = i0 + wm * WM + 16 * a + r;
@@ -503,7 +508,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void skge_fused_kernel(cons
             for (int reg = 0; reg < 4; ++reg) {
                 const int64_t j = j0 + wn * WN + 16 * c + Mfma<T>::drow(lane, reg);
                 if (i < p.M && j < p.N) {
-                    T *dst = C + i + j * p.ldc;
+                    T *dst = C + i + j * ldc;
                     const T v = alpha * acc[a][c][reg];
                     *dst = (beta == (T)0) ? v : v + beta * *dst;
                 }
@@ -739,6 +744,18 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
     }
 }
 
+// split-K: C = sum_z partial[z] + beta C (partials already carry alpha), in a fixed order
+template <typename T>
+__global__ void splitk_reduce_kernel(int64_t M, int64_t N, int split, const T *partial, T beta, T *C, int64_t ldc) {
+    const int64_t total = M * N;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        T v = partial[e];
+        for (int z = 1; z < split; ++z) v += partial[z * total + e];
+        T *c = C + (e % M) + (e / M) * ldc;
+        *c = (beta == (T)0) ? v : v + beta * *c;
+    }
+}
+
 template <typename T>
 __global__ void scale_kernel(int64_t M, int64_t N, T beta, T *C, int64_t ldc) {
     const int64_t total = M * N;
@@ -770,11 +787,36 @@ static hipError_t launch_fused(const GemmProblem &p, hipStream_t s) {
     if (nb <= 0) return hipSuccess;
     // two LDS stages of (BM + BN) rows: 17-element f64 rows keep the 64 x 512 tile under 160 KB
     constexpr int LDK = (sizeof(T) == 8 && BM + BN > 384) ? BK + 1 : Mfma<T>::LDK;
+    // Optional split-K (RBH_SPLITK = s > 1): s workgroups per tile each take 1/s of K and a
+    // deterministic reduction forms C. Measured at C4 (256 workgroups, one per CU): 6.08 ms
+    // unsplit, 6.11 / 6.14 ms with 2 / 4 splits, so it is off by default.
+    static const int split_env = [] { const char *e = getenv("RBH_SPLITK"); return e ? atoi(e) : 0; }();
+    const int64_t nk = (p.K + BK - 1) / BK;
+    int split = 1;
+    if (split_env > 0) split = split_env;
+    if (split > nk) split = (int)(nk > 0 ? nk : 1);
+    GemmProblem q = p;
+    q.splitk = split;
+    q.partial = nullptr;
+    hipError_t e;
+    if (split > 1) {
+        e = hipMallocAsync(&q.partial, sizeof(T) * (size_t)split * p.M * p.N, s);
+        if (e != hipSuccess) return e;
+    }
     timing_begin(s);
-    hipLaunchKernelGGL((skge_fused_kernel<T, XK, YK, FAMILY, BM, BN, WMS, WNS, LDK>), dim3((unsigned)nb),
-                       dim3(64 * WMS * WNS), 0, s, p);
-    hipError_t e = hipGetLastError();
+    hipLaunchKernelGGL((skge_fused_kernel<T, XK, YK, FAMILY, BM, BN, WMS, WNS, LDK>), dim3((unsigned)(nb * split)),
+                       dim3(64 * WMS * WNS), 0, s, q);
+    e = hipGetLastError();
+    if (split > 1 && e == hipSuccess) {
+        hipLaunchKernelGGL(splitk_reduce_kernel<T>, dim3(2048), dim3(256), 0, s, p.M, p.N, split,
+                           (const T *)q.partial, (T)p.beta, (T *)p.C, p.ldc);
+        e = hipGetLastError();
+    }
     timing_end(s);
+    if (split > 1) {
+        hipError_t e2 = hipFreeAsync(q.partial, s);
+        if (e == hipSuccess) e = e2;
+    }
     return e;
 }
 
