@@ -739,9 +739,12 @@ __global__ __launch_bounds__(SU_NT) void saso_unit_kernel(const SparseApply p, c
             uint32_t wa[SU_D], wb[SU_D];
             issue(0, ya, wa);
             const int nsteps = (nw + SU_D - 1) / SU_D;
-#pragma unroll 1
-            for (int s2 = 0; s2 < nsteps; s2 += 2) {
-                // step s2 (ya) has its reads in flight: issue step s2 + 1 (yb), then update
+            // straight-line (a window has at most SU_WIN entries): constant readlane lanes and no
+            // loop-carried wait state; step s2 (ya) has its reads in flight while s2 + 1 issues
+            constexpr int MAXS = (SU_WIN + SU_D - 1) / SU_D;
+#pragma unroll
+            for (int s2 = 0; s2 < MAXS; s2 += 2) {
+                if (s2 >= nsteps) break;
                 issue((s2 + 1) * SU_D, yb, wb);
                 update(ya, wa);
                 if (s2 + 1 >= nsteps) break;
@@ -1021,6 +1024,20 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
             uint32_t wa[SU_D], wb[SU_D];
             issue(0, ya, wa);
             const int nsteps = (nw + SU_D - 1) / SU_D;
+#ifndef SD_LOOP
+            // straight-line walk (a window has at most SU_WIN entries): constant lane indices for
+            // the readlanes, and no loop-carried wait state for the compiler to merge
+            constexpr int MAXS = (SU_WIN + SU_D - 1) / SU_D;
+#pragma unroll
+            for (int s2 = 0; s2 < MAXS; s2 += 2) {
+                if (s2 >= nsteps) break;
+                issue((s2 + 1) * SU_D, yb, wb);
+                update(ya, wa);
+                if (s2 + 1 >= nsteps) break;
+                issue((s2 + 2) * SU_D, ya, wa);
+                update(yb, wb);
+            }
+#else
 #pragma unroll 1
             for (int s2 = 0; s2 < nsteps; s2 += 2) {
                 issue((s2 + 1) * SU_D, yb, wb);
@@ -1029,6 +1046,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
                 issue((s2 + 2) * SU_D, ya, wa);
                 update(yb, wb);
             }
+#endif
         };
         for (int done = 0; done < ne; done += SU_WIN) {
             const int nw = ne - done < SU_WIN ? ne - done : SU_WIN;
