@@ -842,7 +842,7 @@ struct SdAcc {
 #ifdef SD_BATCH
 // four entries in one index-mode section: the row index moves with s_set_gpr_idx_idx, so the mode
 // is toggled once per four adds (the sign flips are done before the section)
-__device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t (&w)[4], const double (&y)[4]) {
+__device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t *w, const double *y) {
     double ys[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -1013,8 +1013,9 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
             };
             auto update = [&](const T (&y)[SU_D], const uint32_t (&w)[SU_D]) {
 #ifdef SD_BATCH
-                static_assert(SU_D == 4, "batched update takes four entries");
-                sd_add4(acc, w, y);
+                static_assert(SU_D % 4 == 0, "batched update takes four entries at a time");
+#pragma unroll
+                for (int g = 0; g < SU_D; g += 4) sd_add4(acc, w + g, y + g);
 #else
 #pragma unroll
                 for (int q = 0; q < SU_D; ++q) acc.add_at(w[q], y[q]);
