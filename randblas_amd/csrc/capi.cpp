@@ -9,6 +9,7 @@
 // works unchanged; device arrays are used in place and the work is stream-ordered.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -110,11 +111,30 @@ struct Staged {
     bool out = false;
 };
 
+// Workspaces come from the device's default stream-ordered pool (hipMallocAsync). With the default
+// release threshold (0) the pool trims its memory at every synchronisation; in a process without
+// torch (a C/C++ client on the default stream) a trimmed-and-reallocated block was observed to
+// read back zeros after a kernel had filled it. Keep the pool's memory: threshold = max, once per
+// device.
+void keep_pool_memory() {
+    static std::atomic<uint64_t> done{0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) { (void)hipGetLastError(); return; }
+    if (done.load() & (1ull << dev)) return;
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+        uint64_t thr = UINT64_MAX;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+    }
+    (void)hipGetLastError();
+    done.fetch_or(1ull << dev);
+}
+
 struct Stager {
     hipStream_t s;
     std::vector<Staged> v;
     bool any_host = false;
-    explicit Stager(hipStream_t st) : s(st) {}
+    explicit Stager(hipStream_t st) : s(st) { keep_pool_memory(); }
     // returns device pointer (or nullptr on error / null input)
     hipError_t map(const void *p, size_t bytes, bool copy_in, bool out, void **dptr) {
         *dptr = nullptr;
@@ -129,7 +149,9 @@ struct Stager {
         hipError_t e = hipMalloc(&st.dev, bytes);
         if (e != hipSuccess) return e;
         if (copy_in) {
+            // pageable source: the copy completes before the call's kernels are queued
             e = hipMemcpyAsync(st.dev, p, bytes, hipMemcpyHostToDevice, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) { (void)hipFree(st.dev); return e; }
         }
         v.push_back(st);
@@ -138,6 +160,11 @@ struct Stager {
     }
     hipError_t finish() {
         hipError_t err = hipSuccess;
+        // host outputs: drain the stream before the pageable D2H copies
+        if (any_host) {
+            hipError_t e = hipStreamSynchronize(s);
+            if (e != hipSuccess) err = e;
+        }
         for (auto &st : v)
             if (st.out) {
                 hipError_t e = hipMemcpyAsync(st.host, st.dev, st.bytes, hipMemcpyDeviceToHost, s);

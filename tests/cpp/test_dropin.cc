@@ -9,6 +9,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <exception>
 #include <cstdlib>
 #include <limits>
 #include <vector>
@@ -254,6 +255,16 @@ static void sparse_data_sketch() {
 }
 
 int main() {
+#ifdef ONLY_SKSP   // diagnostics: the sketch_sparse checks alone
+    try {
+        sparse_data_sketch();
+    } catch (std::exception &e) {
+        std::printf("exception: %s\n", e.what());
+        return 2;
+    }
+    std::printf(g_fail ? "%d checks FAILED\n" : "ALL PASSED\n", g_fail);
+    return g_fail ? 1 : 0;
+#endif
     dense_left<double>(Layout::ColMajor);
     dense_left<double>(Layout::RowMajor);
     dense_left<float>(Layout::ColMajor);
