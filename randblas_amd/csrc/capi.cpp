@@ -486,6 +486,15 @@ hipError_t run_sparse_apply_t<float>(const SparseApply &p, const int64_t *r, con
                                      int64_t nnz, hipStream_t s) {
     return run_sparse_apply_f32(p, r, c, v, nnz, s);
 }
+template <typename T> hipError_t run_sparse_sampled_t(const SparseApply &, const SparseGen &, int64_t, hipStream_t);
+template <>
+hipError_t run_sparse_sampled_t<double>(const SparseApply &p, const SparseGen &g, int64_t nnz, hipStream_t s) {
+    return run_sparse_sampled_f64(p, g, nnz, s);
+}
+template <>
+hipError_t run_sparse_sampled_t<float>(const SparseApply &p, const SparseGen &g, int64_t nnz, hipStream_t s) {
+    return run_sparse_sampled_f32(p, g, nnz, s);
+}
 
 SparseGen make_sparse_gen(const rbh_sparse_dist *D, const rbh_state *seed) {
     SparseGen g{};
@@ -557,32 +566,19 @@ int sparse_common(SparseApply &p, const rbh_sparse_dist *D, const rbh_state *see
     RBH_HIP(st.map(B, sizeof(T) * B_extent, beta != (T)0, true, &dB));
     p.Y = dA;
     p.C = dB;
-    const void *dr = nullptr, *dc = nullptr, *dv = nullptr;
-    void *gen_ws = nullptr;
-    if (!rows) {   // sample the operator on the device
+    if (const char *ab = getenv("RBH_SASO_ABLATE")) p.ablate = atoi(ab);   // diagnostics only
+    if (!rows) {   // sample the operator on the device, inside the apply
         RBH_REQUIRE(seed != nullptr);
-        nnz = sparse_nnz(D);
-        const size_t bytes = (size_t)nnz * (2 * sizeof(int64_t) + sizeof(T));
-        RBH_HIP(hipMallocAsync(&gen_ws, bytes, s));
-        int64_t *gr = (int64_t *)gen_ws;
-        int64_t *gc = gr + nnz;
-        T *gv = (T *)(gc + nnz);
-        RBH_HIP(launch_fill_sparse_t<T>(make_sparse_gen(D, seed), gr, gc, gv, s));
-        dr = gr; dc = gc; dv = gv;
-        p.unit_vals = 1;   // fill_sparse draws values +-1 (sparse_skops.hh:389-413)
+        RBH_HIP(run_sparse_sampled_t<T>(p, make_sparse_gen(D, seed), sparse_nnz(D), s));
     } else {
         RBH_REQUIRE(cols != nullptr && vals != nullptr && nnz >= 0);
         void *t0, *t1, *t2;
         RBH_HIP(st.map(rows, sizeof(int64_t) * nnz, true, false, &t0));
         RBH_HIP(st.map(cols, sizeof(int64_t) * nnz, true, false, &t1));
         RBH_HIP(st.map(vals, sizeof(T) * nnz, true, false, &t2));
-        dr = t0; dc = t1; dv = t2;
+        if (p.alpha == 0.0) nnz = 0;   // left_spmm returns after the beta scaling (:134-135)
+        RBH_HIP(run_sparse_apply_t<T>(p, (const int64_t *)t0, (const int64_t *)t1, (const T *)t2, nnz, s));
     }
-    if (p.alpha == 0.0) nnz = 0;   // left_spmm returns after the beta scaling (:134-135)
-    if (const char *ab = getenv("RBH_SASO_ABLATE")) p.ablate = atoi(ab);   // diagnostics only
-    hipError_t e = run_sparse_apply_t<T>(p, (const int64_t *)dr, (const int64_t *)dc, (const T *)dv, nnz, s);
-    if (gen_ws) (void)hipFreeAsync(gen_ws, s);
-    RBH_HIP(e);
     RBH_HIP(st.finish());
     return RBH_OK;
 }

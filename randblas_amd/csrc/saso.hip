@@ -27,8 +27,12 @@
 #include "saso.hpp"
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 
 namespace rbh {
+
+constexpr int SP_KC = 128;        // contracted indices per chunk (LDS panel depth), section 2
 
 // ------------------------------------------------------------------------------------------
 // 1. fill_sparse
@@ -71,8 +75,70 @@ __global__ void fill_sparse_kernel(uint32_t c0, uint32_t c1, uint32_t c2, uint32
     }
 }
 
+
+// Fast form for vec_nnz <= SF_NZ and dim_major < 2^31 (every SASO/LASO in practice): the draw loop
+// is unrolled, so the swap map lives in registers, and the modulus is 32-bit. The result is the
+// same: rv[0] % (dim_major - j) does not depend on the operand width while dim_major - j < 2^32.
+// Step t of the shuffle leaves work[ell_t] = (old work[t]); position t itself is never read again
+// (later pivots are >= t + 1), so slot t = (ell_t, old work[t]) and the latest slot naming a
+// position holds its value. With MARK the entry is also marked for the sort-free CSR build
+// (section 7), which saves the separate mark pass for an operator sampled inside a sketch call.
+constexpr int SF_NZ = 8;
+__device__ __forceinline__ bool sp_locate_rc(int64_t r, int64_t c, const SparseApply &p, int64_t &v, uint32_t &kk,
+                                             int64_t &i) {
+    const int64_t wr = r - p.ro, wc = c - p.co;
+    if (!(wr >= 0 && wr < p.win_r && wc >= 0 && wc < p.win_c)) return false;
+    i = p.transposed ? wc : wr;
+    const int64_t k = p.transposed ? wr : wc;
+    v = (k / SP_KC) * p.M + i;
+    kk = (uint32_t)(k % SP_KC);
+    return true;
+}
+
+template <typename T, bool MARK>
+__global__ __launch_bounds__(64) void fill_sparse_small_kernel(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                                              uint32_t k0, uint32_t k1, int vec_nnz,
+                                                              uint32_t dim_major, int64_t dim_minor, int maj_is_row,
+                                                              int64_t *idx_major, int64_t *idx_minor, T *vals,
+                                                              SparseApply p, uint32_t *mask) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= dim_minor) return;
+    const uint32_t base[4] = {c0, c1, c2, c3};
+    const int64_t offset = i * vec_nnz;
+    uint32_t ctr[4];
+    rb::ctr_add(base, (uint64_t)offset, ctr);
+    uint32_t ep[SF_NZ], ev[SF_NZ];
+#pragma unroll
+    for (int j = 0; j < SF_NZ; ++j) {
+        if (j >= vec_nnz) break;
+        const rb::u32x4 rv = rb::philox4x32<10>(ctr[0], ctr[1], ctr[2], ctr[3], k0, k1);
+        const uint32_t ell = (uint32_t)j + rv.v[0] % (dim_major - (uint32_t)j);
+        uint32_t wj = (uint32_t)j, wl = ell;
+#pragma unroll
+        for (int t = 0; t < j; ++t) {
+            if (ep[t] == (uint32_t)j) wj = ev[t];
+            if (ep[t] == ell) wl = ev[t];
+        }
+        ep[j] = ell;
+        ev[j] = wj;
+        idx_major[offset + j] = (int64_t)wl;
+        if (vals) vals[offset + j] = (rv.v[1] % 2 == 0) ? (T)1.0 : (T)-1.0;
+        if (idx_minor) idx_minor[offset + j] = i;
+        if (MARK) {
+            int64_t v, ii;
+            uint32_t kk;
+            if (sp_locate_rc(maj_is_row ? (int64_t)wl : i, maj_is_row ? i : (int64_t)wl, p, v, kk, ii))
+                atomicOr(&mask[v * 4 + kk / 32], 1u << (kk % 32));
+        }
+        // ctr_work.incr() (sparse_skops.hh:91): 128-bit add of one
+        ctr[0] += 1u;
+        if (ctr[0] == 0u) { ctr[1] += 1u; if (ctr[1] == 0u) { ctr[2] += 1u; if (ctr[2] == 0u) ctr[3] += 1u; } }
+    }
+}
+
 template <typename T>
-static hipError_t launch_fill_sparse_t(const SparseGen &g, int64_t *rows, int64_t *cols, T *vals, hipStream_t s) {
+static hipError_t launch_fill_sparse_t(const SparseGen &g, int64_t *rows, int64_t *cols, T *vals, hipStream_t s,
+                                       const SparseApply *mark_p = nullptr, uint32_t *mask = nullptr) {
     const int64_t long_ax = g.n_rows > g.n_cols ? g.n_rows : g.n_cols;
     const int64_t short_ax = g.n_rows < g.n_cols ? g.n_rows : g.n_cols;
     const bool is_wide = g.n_rows == short_ax;
@@ -83,6 +149,18 @@ static hipError_t launch_fill_sparse_t(const SparseGen &g, int64_t *rows, int64_
     if (g.major_axis == 'S') { dim_major = short_ax; dim_minor = long_ax; imaj = short_idx; imin = long_idx; }
     else { dim_major = long_ax; dim_minor = short_ax; imaj = long_idx; imin = short_idx; }
     if (dim_minor <= 0) return hipSuccess;
+    if (g.vec_nnz <= SF_NZ && dim_major < ((int64_t)1 << 31)) {
+        const unsigned b64 = (unsigned)((dim_minor + 63) / 64);
+        const SparseApply none{};
+        if (mask) hipLaunchKernelGGL((fill_sparse_small_kernel<T, true>), dim3(b64), dim3(64), 0, s, g.ctr[0], g.ctr[1],
+                                    g.ctr[2], g.ctr[3], g.key[0], g.key[1], (int)g.vec_nnz, (uint32_t)dim_major,
+                                    dim_minor, (int)(g.major_axis == 'S' ? is_wide : !is_wide), imaj, imin, vals, *mark_p, mask);
+        else hipLaunchKernelGGL((fill_sparse_small_kernel<T, false>), dim3(b64), dim3(64), 0, s, g.ctr[0], g.ctr[1],
+                                g.ctr[2], g.ctr[3], g.key[0], g.key[1], (int)g.vec_nnz, (uint32_t)dim_major,
+                                dim_minor, (int)(g.major_axis == 'S' ? is_wide : !is_wide), imaj, imin, vals, none, (uint32_t *)nullptr);
+        return hipGetLastError();
+    }
+    if (mask) return hipErrorInvalidValue;   // the fused mark exists only in the fast form
     const unsigned blocks = (unsigned)((dim_minor + 255) / 256);
 #define RBH_FS(MAXN)                                                                                        \
     hipLaunchKernelGGL((fill_sparse_kernel<T, MAXN>), dim3(blocks), dim3(256), 0, s, g.ctr[0], g.ctr[1],   \
@@ -109,7 +187,7 @@ hipError_t launch_fill_sparse_f32(const SparseGen &g, int64_t *rows, int64_t *co
 //    entries of output row i inside chunk c are contiguous and ascending in k, and walking the
 //    chunks in order walks every row in ascending k: the reference's accumulation order.
 // ------------------------------------------------------------------------------------------
-constexpr int SP_KC = 128;        // contracted indices per chunk (LDS panel depth)
+// SP_KC (contracted indices per chunk, the LDS panel depth) is defined at the top of the namespace
 
 // Magnitude test for the uniform-value apply (section 4): UniformTest.mixed is set unless every
 // in-window value alpha*v has the magnitude c = |alpha*vals[0]| (finite, nonzero), which holds for
@@ -1093,14 +1171,18 @@ hipError_t launch_expand_ptr(int64_t n_major, const int64_t *ptr, int64_t *out, 
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ bool sp_locate(int64_t e, const int64_t *rows, const int64_t *cols, const SparseApply &p,
                                           int64_t &v, uint32_t &kk, int64_t &i) {
-    const int64_t wr = rows[e] - p.ro, wc = cols[e] - p.co;
-    if (!(wr >= 0 && wr < p.win_r && wc >= 0 && wc < p.win_c)) return false;
-    i = p.transposed ? wc : wr;
-    const int64_t k = p.transposed ? wr : wc;
-    v = (k / SP_KC) * p.M + i;
-    kk = (uint32_t)(k % SP_KC);
-    return true;
+    return sp_locate_rc(rows[e], cols[e], p, v, kk, i);
 }
+
+// entries of virtual row v (v == NV: the scan's closing zero), read by the scan itself
+struct MaskPopcount {
+    const uint32_t *mask;
+    int64_t NV;
+    __device__ __host__ int32_t operator()(int64_t v) const {
+        return v < NV ? __popc(mask[4 * v]) + __popc(mask[4 * v + 1]) + __popc(mask[4 * v + 2]) + __popc(mask[4 * v + 3])
+                      : 0;
+    }
+};
 
 __global__ void mark_kernel(int64_t nnz, const int64_t *rows, const int64_t *cols, const SparseApply p,
                             uint32_t *mask) {
@@ -1108,13 +1190,6 @@ __global__ void mark_kernel(int64_t nnz, const int64_t *rows, const int64_t *col
     int64_t v, i;
     uint32_t kk;
     if (e < nnz && sp_locate(e, rows, cols, p, v, kk, i)) atomicOr(&mask[v * 4 + kk / 32], 1u << (kk % 32));
-}
-
-__global__ void mask_count_kernel(int64_t NV, const uint32_t *mask, int32_t *cnt) {
-    const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (v > NV) return;
-    cnt[v] = v < NV ? __popc(mask[4 * v]) + __popc(mask[4 * v + 1]) + __popc(mask[4 * v + 2]) + __popc(mask[4 * v + 3])
-                    : 0;
 }
 
 template <typename T>
@@ -1132,36 +1207,49 @@ __global__ void place_kernel(int64_t nnz, const int64_t *rows, const int64_t *co
     rec[vrp[v] + rank] = (sizeof(T) == 8 ? 2u * row : row) | ((kk * kmul) << 8) | (signbit(x) ? 0x80000000u : 0u);
 }
 
-// The LDS-DMA apply (section 5) on a sort-free CSR.
-static hipError_t run_sparse_dma(const SparseApply &p, const int64_t *rows, const int64_t *cols, const double *vals,
-                                 int64_t nnz, bool y_k, hipStream_t s) {
+// The LDS-DMA apply (section 5) on a sort-free CSR. With gen, the operator is sampled here into
+// the workspace and its entries marked in the same pass (fill_sparse_small_kernel<.., true>).
+static hipError_t run_sparse_dma(const SparseApply &p, const SparseGen *gen, const int64_t *rows, const int64_t *cols,
+                                 const double *vals, int64_t nnz, bool y_k, hipStream_t s) {
     const int64_t nchunks = p.K > 0 ? (p.K + SP_KC - 1) / SP_KC : 0;
     const int64_t NV = nchunks * p.M;
     const size_t n = (size_t)(nnz > 0 ? nnz : 1);
+    const MaskPopcount pc0{nullptr, NV};
+    auto cnt_it0 = rocprim::make_transform_iterator(rocprim::counting_iterator<int64_t>(0), pc0);
     size_t scan_bytes = 0;
-    hipError_t err = rocprim::exclusive_scan(nullptr, scan_bytes, (const int32_t *)nullptr, (int32_t *)nullptr, 0,
-                                             (size_t)(NV + 1), rocprim::plus<int32_t>(), s);
+    hipError_t err = rocprim::exclusive_scan(nullptr, scan_bytes, cnt_it0, (int32_t *)nullptr, 0, (size_t)(NV + 1),
+                                             rocprim::plus<int32_t>(), s);
     if (err != hipSuccess) return err;
-    const size_t bytes = (size_t)NV * 16 + 2 * (size_t)(NV + 1) * sizeof(int32_t) + n * sizeof(uint32_t) + scan_bytes + 256;
+    const size_t gen_bytes = gen ? n * (2 * sizeof(int64_t) + sizeof(double)) + 64 : 0;
+    const size_t bytes = (size_t)NV * 16 + (size_t)(NV + 1) * sizeof(int32_t) + n * sizeof(uint32_t) + scan_bytes +
+                         gen_bytes + 256;
     char *ws = nullptr;
     err = hipMallocAsync((void **)&ws, bytes, s);
     if (err != hipSuccess) return err;
     size_t off = 0;
     auto carve = [&](size_t b) { void *q = ws + off; off += (b + 15) & ~(size_t)15; return q; };
     uint32_t *mask = (uint32_t *)carve((size_t)NV * 16);
-    int32_t *cnt = (int32_t *)carve((size_t)(NV + 1) * sizeof(int32_t));
     int32_t *vrp = (int32_t *)carve((size_t)(NV + 1) * sizeof(int32_t));
     uint32_t *rec = (uint32_t *)carve(n * sizeof(uint32_t));
     void *tmp = carve(scan_bytes);
+    if (gen) {
+        int64_t *gr = (int64_t *)carve(n * sizeof(int64_t));
+        int64_t *gc = (int64_t *)carve(n * sizeof(int64_t));
+        double *gv = (double *)carve(n * sizeof(double));
+        rows = gr; cols = gc; vals = gv;
+    }
     const uint32_t kmul = y_k ? (uint32_t)sizeof(double) : (uint32_t)(SU_J * sizeof(double));
     err = hipMemsetAsync(mask, 0, (size_t)NV * 16, s);
-    if (err == hipSuccess && nnz > 0) {
+    if (err == hipSuccess && gen) {
+        err = launch_fill_sparse_t<double>(*gen, (int64_t *)rows, (int64_t *)cols, (double *)vals, s, &p, mask);
+    } else if (err == hipSuccess && nnz > 0) {
         hipLaunchKernelGGL(mark_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, rows, cols, p, mask);
         err = hipGetLastError();
     }
     if (err == hipSuccess) {
-        hipLaunchKernelGGL(mask_count_kernel, dim3((unsigned)((NV + 1 + 255) / 256)), dim3(256), 0, s, NV, mask, cnt);
-        err = rocprim::exclusive_scan(tmp, scan_bytes, cnt, vrp, 0, (size_t)(NV + 1), rocprim::plus<int32_t>(), s);
+        const MaskPopcount pc{mask, NV};
+        auto cnt_it = rocprim::make_transform_iterator(rocprim::counting_iterator<int64_t>(0), pc);
+        err = rocprim::exclusive_scan(tmp, scan_bytes, cnt_it, vrp, 0, (size_t)(NV + 1), rocprim::plus<int32_t>(), s);
     }
     if (err == hipSuccess && nnz > 0) {
         hipLaunchKernelGGL(place_kernel<double>, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, rows, cols,
@@ -1182,19 +1270,25 @@ static hipError_t run_sparse_dma(const SparseApply &p, const int64_t *rows, cons
     return err != hipSuccess ? err : e2;
 }
 
+// The DMA kernel's conditions: f64, values +-1 (sampled operator: distinct entries), |alpha| = 1
+// (the panel is Y itself), Y contiguous along k or j in 16-B vectors.
+static bool dma_eligible(const SparseApply &p, bool &y_k) {
+    static const bool dma_off = [] { const char *e = getenv("RBH_NO_SASO_DMA"); return e && e[0] == '1'; }();
+    constexpr int VEC = 2;
+    y_k = p.ysk == 1 && (p.ysj % VEC) == 0 && (((uintptr_t)p.Y) % 16) == 0 && (p.K % VEC) == 0;
+    const bool y_jd = p.ysj == 1 && (p.ysk % VEC) == 0 && (((uintptr_t)p.Y) % 16) == 0 && (p.N % VEC) == 0;
+    return p.unit_vals && (p.alpha == 1.0 || p.alpha == -1.0) && (y_k || y_jd) && !dma_off;
+}
+
 template <typename T>
 static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, const int64_t *cols, const T *vals,
                                      int64_t nnz, hipStream_t s) {
     if (p.M <= 0 || p.N <= 0) return hipSuccess;
     if (nnz >= (int64_t)0x7fffffff) return hipErrorInvalidValue;
-    {   // LDS-DMA kernel (section 5) on the sort-free CSR (section 7): f64, values +-1 (operator
-        // sampled in this call: distinct entries), |alpha| = 1
-        constexpr int VEC = SuCfg<T>::VEC;
-        static const bool dma_off = [] { const char *e = getenv("RBH_NO_SASO_DMA"); return e && e[0] == '1'; }();
-        const bool y_k = p.ysk == 1 && (p.ysj % VEC) == 0 && (((uintptr_t)p.Y) % 16) == 0 && (p.K % VEC) == 0;
-        const bool y_jd = p.ysj == 1 && (p.ysk % VEC) == 0 && (((uintptr_t)p.Y) % 16) == 0 && (p.N % VEC) == 0;
-        if (sizeof(T) == 8 && p.unit_vals && (p.alpha == 1.0 || p.alpha == -1.0) && (y_k || y_jd) && !dma_off)
-            return run_sparse_dma(p, rows, cols, (const double *)vals, nnz, y_k, s);
+    {   // LDS-DMA kernel (section 5) on the sort-free CSR (section 7)
+        bool y_k;
+        if (sizeof(T) == 8 && dma_eligible(p, y_k))
+            return run_sparse_dma(p, nullptr, rows, cols, (const double *)vals, nnz, y_k, s);
     }
     hipError_t err;
     const int64_t nchunks = p.K > 0 ? (p.K + SP_KC - 1) / SP_KC : 0;
@@ -1274,6 +1368,41 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
     timing_end(s);
     hipError_t e2 = hipFreeAsync(ws, s);
     return err != hipSuccess ? err : e2;
+}
+
+// A sparse sketch whose operator is sampled in the call (SparseSkOp without arrays): sample and
+// apply. On the DMA path the sampling also marks the CSR entries (one pass fewer); otherwise the
+// operator is sampled into a workspace and takes the general apply.
+template <typename T>
+static hipError_t run_sparse_sampled_t(const SparseApply &p0, const SparseGen &g, int64_t nnz, hipStream_t s) {
+    SparseApply p = p0;
+    p.unit_vals = 1;   // fill_sparse draws values +-1 (sparse_skops.hh:389-413)
+    const int64_t long_ax = g.n_rows > g.n_cols ? g.n_rows : g.n_cols;
+    const int64_t short_ax = g.n_rows < g.n_cols ? g.n_rows : g.n_cols;
+    const int64_t dim_major = g.major_axis == 'S' ? short_ax : long_ax;
+    bool y_k = false;
+    if (sizeof(T) == 8 && p.M > 0 && p.N > 0 && nnz > 0 && g.vec_nnz <= SF_NZ && dim_major < ((int64_t)1 << 31) &&
+        dma_eligible(p, y_k))
+        return run_sparse_dma(p, &g, nullptr, nullptr, nullptr, nnz, y_k, s);
+    const size_t n = (size_t)(nnz > 0 ? nnz : 1);
+    char *ws = nullptr;
+    hipError_t err = hipMallocAsync((void **)&ws, n * (2 * sizeof(int64_t) + sizeof(T)), s);
+    if (err != hipSuccess) return err;
+    int64_t *gr = (int64_t *)ws;
+    int64_t *gc = gr + n;
+    T *gv = (T *)(gc + n);
+    err = launch_fill_sparse_t<T>(g, gr, gc, gv, s);
+    // left_spmm returns after the beta scaling when alpha == 0 (spmm_dispatch.hh:134-135)
+    if (err == hipSuccess) err = run_sparse_apply_t<T>(p, gr, gc, gv, p.alpha == 0.0 ? 0 : nnz, s);
+    hipError_t e2 = hipFreeAsync(ws, s);
+    return err != hipSuccess ? err : e2;
+}
+
+hipError_t run_sparse_sampled_f64(const SparseApply &p, const SparseGen &g, int64_t nnz, hipStream_t s) {
+    return run_sparse_sampled_t<double>(p, g, nnz, s);
+}
+hipError_t run_sparse_sampled_f32(const SparseApply &p, const SparseGen &g, int64_t nnz, hipStream_t s) {
+    return run_sparse_sampled_t<float>(p, g, nnz, s);
 }
 
 hipError_t run_sparse_apply_f64(const SparseApply &p, const int64_t *rows, const int64_t *cols, const double *vals,

@@ -36,6 +36,10 @@ hipError_t run_sparse_apply_f64(const SparseApply &p, const int64_t *rows, const
 hipError_t run_sparse_apply_f32(const SparseApply &p, const int64_t *rows, const int64_t *cols, const float *vals,
                                 int64_t nnz, hipStream_t s);
 
+// Sample the operator (SparseGen, nnz entries) on the device and apply it: C = beta*C + op'(S) Y.
+hipError_t run_sparse_sampled_f64(const SparseApply &p, const SparseGen &g, int64_t nnz, hipStream_t s);
+hipError_t run_sparse_sampled_f32(const SparseApply &p, const SparseGen &g, int64_t nnz, hipStream_t s);
+
 // CSR/CSC pointer array (n_major + 1 entries) -> the major index of every entry (saso.hip).
 hipError_t launch_expand_ptr(int64_t n_major, const int64_t *ptr, int64_t *out, hipStream_t s);
 
