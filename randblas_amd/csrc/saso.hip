@@ -870,10 +870,15 @@ __global__ __launch_bounds__(SU_NT) void saso_unit_kernel(const SparseApply p, c
 //        koff = k * sizeof(T).
 //      * Y contiguous along j (YJ = true): [SP_KC][64 columns]; koff = k * 64 * sizeof(T).
 //    Padding records add into a dummy accumulator register (v[96:97]), so no zero element.
-//    The workgroup's records of a chunk are one contiguous CSR range; up to SD_RCAP of them are
-//    staged (mean at C3: 512), the rest are read from HBM before their window.
+//    A wave's records of a chunk are one contiguous CSR range. By default they are read with
+//    scalar loads (s_load_dwordx8 x 4) straight into SGPRs, SD_SW per window, so an entry costs
+//    three VALU (address, sign, add) and three SALU ops, no readlane; the last one to three
+//    entries of a window are padded to a batch of four. Measured at C3: 0.731 -> 0.677 ms.
+//    With -DSD_NO_SMEM the workgroup's records are staged in LDS instead (up to SD_RCAP, mean at
+//    C3: 512; the rest read from HBM before their window) and taken with v_readlane.
 // ------------------------------------------------------------------------------------------
 constexpr int SD_RCAP = 2048;
+constexpr int SD_SW = 32;   // records per scalar-load window (default walk; -DSD_NO_SMEM: LDS records + readlane)
 // LDS reads of the walk stay in flight across the index-mode add (measured: no effect on the
 // results, 6 % faster than draining them); -DSD_DRAIN_LDS restores the drain
 #ifdef SD_DRAIN_LDS
@@ -920,6 +925,34 @@ struct SdAcc {
 #ifdef SD_BATCH
 // four entries in one index-mode section: the row index moves with s_set_gpr_idx_idx, so the mode
 // is toggled once per four adds (the sign flips are done before the section)
+#ifdef SD_FMA
+// sign on the scalar side: fma(y, +-1.0, acc) rounds once, exactly as acc + (+-y), so the entry
+// costs one VALU op (the +-1.0 pair is built by SALU from the record's sign bit)
+__device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t *w, const double *y) {
+    uint64_t sg[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint32_t hi;
+        asm("s_and_b32 %0, %1, 0x80000000\n\t"
+            "s_or_b32 %0, %0, 0x3ff00000"
+            : "=&s"(hi) : "s"(w[q]) : "scc");
+        sg[q] = (uint64_t)hi << 32;
+    }
+    asm volatile("s_set_gpr_idx_on %3, gpr_idx(SRC2,DST)\n\t"
+                 "v_fma_f64 v[32:33], %7, %11, v[32:33]\n\t"
+                 "s_set_gpr_idx_idx %4\n\t"
+                 "v_fma_f64 v[32:33], %8, %12, v[32:33]\n\t"
+                 "s_set_gpr_idx_idx %5\n\t"
+                 "v_fma_f64 v[32:33], %9, %13, v[32:33]\n\t"
+                 "s_set_gpr_idx_idx %6\n\t"
+                 "v_fma_f64 v[32:33], %10, %14, v[32:33]\n\t"
+                 "s_set_gpr_idx_off"
+                 : "+{v[32:63]}"(acc.a), "+{v[64:95]}"(acc.b), "+{v[96:97]}"(acc.dmy)
+                 : "s"(w[0]), "s"(w[1]), "s"(w[2]), "s"(w[3]), "v"(y[0]), "v"(y[1]), "v"(y[2]), "v"(y[3]),
+                   "s"(sg[0]), "s"(sg[1]), "s"(sg[2]), "s"(sg[3])
+                 : "m0", "scc");
+}
+#else
 __device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t *w, const double *y) {
     double ys[4];
 #pragma unroll
@@ -941,6 +974,7 @@ __device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t *w, const dou
                  : "s"(w[0]), "s"(w[1]), "s"(w[2]), "s"(w[3]), "v"(ys[0]), "v"(ys[1]), "v"(ys[2]), "v"(ys[3])
                  : "m0", "scc");
 }
+#endif
 #endif
 
 __device__ __forceinline__ uint32_t lds_addr(const void *ptr) {
@@ -1060,7 +1094,9 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     if (nchunks > 1) dma_bounds(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+#ifdef SD_NO_SMEM
     dma_recs(0);
+#endif
     dma_panel(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1069,8 +1105,10 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
                                  : lane * (uint32_t)(SP_KC * sizeof(T)) + 16u * (lane & 15u);
     for (int64_t ch = 0; ch < nchunks; ++ch) {
         if (ch + 1 < nchunks) {
+#ifdef SD_NO_SMEM
             dma_recs(ch + 1);
-            dma_panel(ch + 1);
+#endif
+            if (!(p.ablate & 2)) dma_panel(ch + 1);   // diagnostics: ablate 2 skips the panel copies
         }
         if (ch + 2 < nchunks) dma_bounds(ch + 2);
         const int32_t *bb = bnd + (ch & 3) * 64;
@@ -1081,6 +1119,19 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
         ne = ne < 0 ? 0 : (ne > SU_R * SP_KC ? SU_R * SP_KC : ne);
         const uint32_t L = lanebase + (uint32_t)((ch & 1) * G::PANEL_B);
         const uint32_t *rbuf = recs + (ch & 1) * SD_RCAP;
+#ifndef SD_NO_SMEM
+        // records come straight from HBM/L2 into SGPRs (scalar loads), one window at a time: no
+        // readlane per entry. Entries past the window's end are padding records.
+        auto walk = [&](const uint32_t (&wr)[SD_SW], int nw) {
+            auto issue = [&](int x0, T (&y)[SU_D], uint32_t (&w)[SU_D]) {
+#pragma unroll
+                for (int q = 0; q < SU_D; ++q) {
+                    w[q] = x0 + q < SD_SW ? wr[x0 + q < SD_SW ? x0 + q : 0] : G::PAD;
+                    y[q] = *reinterpret_cast<const T *>(lbase + (L ^ ((w[q] >> 8) & 0xfffffu)));
+                }
+            };
+            constexpr int WIN = SD_SW;
+#else
         auto walk = [&](uint32_t rc, int nw) {
             auto issue = [&](int x0, T (&y)[SU_D], uint32_t (&w)[SU_D]) {
 #pragma unroll
@@ -1089,6 +1140,8 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
                     y[q] = *reinterpret_cast<const T *>(lbase + (L ^ ((w[q] >> 8) & 0xfffffu)));
                 }
             };
+            constexpr int WIN = SU_WIN;
+#endif
             auto update = [&](const T (&y)[SU_D], const uint32_t (&w)[SU_D]) {
 #ifdef SD_BATCH
                 static_assert(SU_D % 4 == 0, "batched update takes four entries at a time");
@@ -1106,7 +1159,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
 #ifndef SD_LOOP
             // straight-line walk (a window has at most SU_WIN entries): constant lane indices for
             // the readlanes, and no loop-carried wait state for the compiler to merge
-            constexpr int MAXS = (SU_WIN + SU_D - 1) / SU_D;
+            constexpr int MAXS = (WIN + SU_D - 1) / SU_D;
 #pragma unroll
             for (int s2 = 0; s2 < MAXS; s2 += 2) {
                 if (s2 >= nsteps) break;
@@ -1127,6 +1180,47 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
             }
 #endif
         };
+        if (p.ablate & 1) ne = 0;   // diagnostics: ablate 1 skips the walk
+#ifndef SD_NO_SMEM
+        for (int done = 0; done < ne; done += SD_SW) {
+            const int nw = ne - done < SD_SW ? ne - done : SD_SW;
+            const uint32_t *gw = rec32 + B0 + eb + done;   // rec32 is padded by SD_SW records
+            typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+            u32x8 r0, r1, r2, r3;
+            asm volatile("s_load_dwordx8 %0, %4, 0x0\n\t"
+                         "s_load_dwordx8 %1, %4, 0x20\n\t"
+                         "s_load_dwordx8 %2, %4, 0x40\n\t"
+                         "s_load_dwordx8 %3, %4, 0x60\n\t"
+                         "s_waitcnt lgkmcnt(0)"
+                         : "=&s"(r0), "=&s"(r1), "=&s"(r2), "=&s"(r3)
+                         : "s"(gw)
+                         : "memory");
+            uint32_t wr[SD_SW];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) { wr[q] = r0[q]; wr[8 + q] = r1[q]; wr[16 + q] = r2[q]; wr[24 + q] = r3[q]; }
+            // whole steps of four straight from the window, no per-entry selects (an issue past
+            // the last step reads a stale record's LDS slot, which no add uses)
+            const int nfull = nw & ~3;
+            if (nfull > 0) walk(wr, nfull);
+            if (nw & 3) {   // the last one to three entries, padded to a step of four
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                u32x4 rt;
+                asm volatile("s_load_dwordx4 %0, %1, 0x0\n\t"
+                             "s_waitcnt lgkmcnt(0)"
+                             : "=&s"(rt)
+                             : "s"(gw + nfull)
+                             : "memory");
+                uint32_t w4[4];
+                T y4[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    w4[q] = q < (nw & 3) ? rt[q] : G::PAD;
+                    y4[q] = *reinterpret_cast<const T *>(lbase + (L ^ ((w4[q] >> 8) & 0xfffffu)));
+                }
+                sd_add4(acc, w4, y4);
+            }
+        }
+#else
         for (int done = 0; done < ne; done += SU_WIN) {
             const int nw = ne - done < SU_WIN ? ne - done : SU_WIN;
             const int rel = eb + done + (int)lane;
@@ -1141,6 +1235,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
             }
             walk(rc, nw);
         }
+#endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
@@ -1221,7 +1316,7 @@ static hipError_t run_sparse_dma(const SparseApply &p, const SparseGen *gen, con
                                              rocprim::plus<int32_t>(), s);
     if (err != hipSuccess) return err;
     const size_t gen_bytes = gen ? n * (2 * sizeof(int64_t) + sizeof(double)) + 64 : 0;
-    const size_t bytes = (size_t)NV * 16 + (size_t)(NV + 1) * sizeof(int32_t) + n * sizeof(uint32_t) + scan_bytes +
+    const size_t bytes = (size_t)NV * 16 + (size_t)(NV + 1) * sizeof(int32_t) + (n + SD_SW) * sizeof(uint32_t) + scan_bytes +
                          gen_bytes + 256;
     char *ws = nullptr;
     err = hipMallocAsync((void **)&ws, bytes, s);
@@ -1230,7 +1325,7 @@ static hipError_t run_sparse_dma(const SparseApply &p, const SparseGen *gen, con
     auto carve = [&](size_t b) { void *q = ws + off; off += (b + 15) & ~(size_t)15; return q; };
     uint32_t *mask = (uint32_t *)carve((size_t)NV * 16);
     int32_t *vrp = (int32_t *)carve((size_t)(NV + 1) * sizeof(int32_t));
-    uint32_t *rec = (uint32_t *)carve(n * sizeof(uint32_t));
+    uint32_t *rec = (uint32_t *)carve((n + SD_SW) * sizeof(uint32_t));   // + scalar-window overrun
     void *tmp = carve(scan_bytes);
     if (gen) {
         int64_t *gr = (int64_t *)carve(n * sizeof(int64_t));
