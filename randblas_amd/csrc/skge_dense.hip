@@ -864,10 +864,15 @@ static hipError_t launch_gemm(const GemmProblem &p, hipStream_t s) {
     if (fused_ok(p)) {
         // tile (generated x memory outer indices) and waves; f32 variants selectable for tuning
 #ifndef RBH_F32_TG
-#define RBH_F32_TG 128
-#define RBH_F32_TM 256
-#define RBH_F32_WG 2
-#define RBH_F32_WMW 4
+// f32 (C4): 64 generated x 512 memory rows, one wave along the generated dimension. Each operator
+// entry is drawn once per 512 memory columns instead of 256, for the same 64 accumulators per
+// lane. Measured at C4 (d = 256 per GPU, m = n = 32768): 128 x 256 / 2 x 4 waves 6.10 ms,
+// 64 x 512 / 1 x 8 waves 5.46 ms, 64 x 512 / 1 x 4 waves 7.93 ms, 128 x 512 / 2 x 8 waves 9.91 ms;
+// 1024-wide tiles exceed the 160 KB of LDS.
+#define RBH_F32_TG 64
+#define RBH_F32_TM 512
+#define RBH_F32_WG 1
+#define RBH_F32_WMW 8
 #endif
         constexpr bool F32 = sizeof(T) == 4;
         constexpr int TG = F32 ? RBH_F32_TG : 128, TMW = F32 ? RBH_F32_TM : 256;
