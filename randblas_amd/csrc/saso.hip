@@ -871,14 +871,17 @@ __global__ __launch_bounds__(SU_NT) void saso_unit_kernel(const SparseApply p, c
 //      * Y contiguous along j (YJ = true): [SP_KC][64 columns]; koff = k * 64 * sizeof(T).
 //    Padding records add into a dummy accumulator register (v[96:97]), so no zero element.
 //    A wave's records of a chunk are one contiguous CSR range. By default they are read with
-//    scalar loads (s_load_dwordx8 x 4) straight into SGPRs, SD_SW per window, so an entry costs
+//    scalar loads (s_load_dwordx8 x 6) straight into SGPRs, SD_SW = 48 per window, so an entry costs
 //    three VALU (address, sign, add) and three SALU ops, no readlane; the last one to three
 //    entries of a window are padded to a batch of four. Measured at C3: 0.731 -> 0.677 ms.
 //    With -DSD_NO_SMEM the workgroup's records are staged in LDS instead (up to SD_RCAP, mean at
 //    C3: 512; the rest read from HBM before their window) and taken with v_readlane.
 // ------------------------------------------------------------------------------------------
 constexpr int SD_RCAP = 2048;
-constexpr int SD_SW = 32;   // records per scalar-load window (default walk; -DSD_NO_SMEM: LDS records + readlane)
+#ifndef SD_SW_DEF
+#define SD_SW_DEF 48   // C3: 0.708 ms with 32-record windows, 0.692 ms with 48 (one window for most waves)
+#endif
+constexpr int SD_SW = SD_SW_DEF;   // records per scalar-load window (32 or 48) (default walk; -DSD_NO_SMEM: LDS records + readlane)
 // LDS reads of the walk stay in flight across the index-mode add (measured: no effect on the
 // results, 6 % faster than draining them); -DSD_DRAIN_LDS restores the drain
 #ifdef SD_DRAIN_LDS
@@ -922,13 +925,16 @@ struct SdAcc {
 #ifndef SD_NO_BATCH
 #define SD_BATCH 1
 #endif
+#ifndef SD_PRE
+#define SD_PRE ""   // diagnostics: an instruction string placed before the index-mode section
+#endif
 #ifdef SD_BATCH
 // four entries in one index-mode section: the row index moves with s_set_gpr_idx_idx, so the mode
 // is toggled once per four adds (the sign flips are done before the section)
 #ifdef SD_FMA
 // sign on the scalar side: fma(y, +-1.0, acc) rounds once, exactly as acc + (+-y), so the entry
 // costs one VALU op (the +-1.0 pair is built by SALU from the record's sign bit)
-__device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t *w, const double *y) {
+__device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t *w, const double *y, uint32_t cm) {
     uint64_t sg[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -953,15 +959,25 @@ __device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t *w, const dou
                  : "m0", "scc");
 }
 #else
-__device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t *w, const double *y) {
+__device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t *w, const double *y, uint32_t cm) {
     double ys[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         uint32_t m;
+#ifdef SD_VSIGN
+        // sign on the vector side: hi ^ (record & 0x80000000) in one v_bitop3 (table 0x78 =
+        // S0 ^ (S1 & S2)), no SALU op
+        (void)m;   // cm: 0x80000000 in a VGPR, materialised once by the kernel
+        const uint64_t yb = __builtin_bit_cast(uint64_t, y[q]);
+        uint32_t hi = (uint32_t)(yb >> 32);
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x78" : "=v"(hi) : "v"(hi), "s"(w[q]), "v"(cm));
+        ys[q] = __builtin_bit_cast(double, ((uint64_t)hi << 32) | (yb & 0xffffffffull));
+#else
         asm("s_and_b32 %0, %1, 0x80000000" : "=s"(m) : "s"(w[q]) : "scc");
         ys[q] = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, y[q]) ^ ((uint64_t)m << 32));
+#endif
     }
-    asm volatile("s_set_gpr_idx_on %3, gpr_idx(SRC0,DST)\n\t"
+    asm volatile(SD_PRE "s_set_gpr_idx_on %3, gpr_idx(SRC0,DST)\n\t"
                  "v_add_f64 v[32:33], v[32:33], %7\n\t"
                  "s_set_gpr_idx_idx %4\n\t"
                  "v_add_f64 v[32:33], v[32:33], %8\n\t"
@@ -1025,6 +1041,8 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     const T *Y = (const T *)p.Y;
     const T beta = (T)p.beta;
 
+    uint32_t sgnmask = 0x80000000u;   // sign-bit mask in a VGPR (SD_VSIGN)
+    asm volatile("" : "+v"(sgnmask));
     SdAcc acc;
     acc.dmy = (T)0;
     if (beta != (T)0) {
@@ -1146,7 +1164,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
 #ifdef SD_BATCH
                 static_assert(SU_D % 4 == 0, "batched update takes four entries at a time");
 #pragma unroll
-                for (int g = 0; g < SU_D; g += 4) sd_add4(acc, w + g, y + g);
+                for (int g = 0; g < SU_D; g += 4) sd_add4(acc, w + g, y + g, sgnmask);
 #else
 #pragma unroll
                 for (int q = 0; q < SU_D; ++q) acc.add_at(w[q], y[q]);
@@ -1198,6 +1216,17 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
             uint32_t wr[SD_SW];
 #pragma unroll
             for (int q = 0; q < 8; ++q) { wr[q] = r0[q]; wr[8 + q] = r1[q]; wr[16 + q] = r2[q]; wr[24 + q] = r3[q]; }
+            if constexpr (SD_SW == 48) {
+                u32x8 r4, r5;
+                asm volatile("s_load_dwordx8 %0, %2, 0x80\n\t"
+                             "s_load_dwordx8 %1, %2, 0xa0\n\t"
+                             "s_waitcnt lgkmcnt(0)"
+                             : "=&s"(r4), "=&s"(r5)
+                             : "s"(gw)
+                             : "memory");
+#pragma unroll
+                for (int q = 0; q < 8; ++q) { wr[32 + q] = r4[q]; wr[40 + q] = r5[q]; }
+            }
             // whole steps of four straight from the window, no per-entry selects (an issue past
             // the last step reads a stale record's LDS slot, which no add uses)
             const int nfull = nw & ~3;
@@ -1217,7 +1246,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
                     w4[q] = q < (nw & 3) ? rt[q] : G::PAD;
                     y4[q] = *reinterpret_cast<const T *>(lbase + (L ^ ((w4[q] >> 8) & 0xfffffu)));
                 }
-                sd_add4(acc, w4, y4);
+                sd_add4(acc, w4, y4, sgnmask);
             }
         }
 #else
