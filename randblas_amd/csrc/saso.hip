@@ -881,7 +881,12 @@ constexpr int SD_RCAP = 2048;
 #ifndef SD_SW_DEF
 #define SD_SW_DEF 48   // C3: 0.708 ms with 32-record windows, 0.692 ms with 48 (one window for most waves)
 #endif
-constexpr int SD_SW = SD_SW_DEF;   // records per scalar-load window (32 or 48) (default walk; -DSD_NO_SMEM: LDS records + readlane)
+constexpr int SD_SW = SD_SW_DEF;   // records per scalar-load window (32 or 48)
+#if SD_SW_DEF == 48
+#define SD_W32 ""
+#else
+#define SD_W32 "s_waitcnt lgkmcnt(0)"
+#endif (default walk; -DSD_NO_SMEM: LDS records + readlane)
 // LDS reads of the walk stay in flight across the index-mode add (measured: no effect on the
 // results, 6 % faster than draining them); -DSD_DRAIN_LDS restores the drain
 #ifdef SD_DRAIN_LDS
@@ -1209,24 +1214,26 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
                          "s_load_dwordx8 %1, %4, 0x20\n\t"
                          "s_load_dwordx8 %2, %4, 0x40\n\t"
                          "s_load_dwordx8 %3, %4, 0x60\n\t"
-                         "s_waitcnt lgkmcnt(0)"
+                         SD_W32
                          : "=&s"(r0), "=&s"(r1), "=&s"(r2), "=&s"(r3)
                          : "s"(gw)
                          : "memory");
             uint32_t wr[SD_SW];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) { wr[q] = r0[q]; wr[8 + q] = r1[q]; wr[16 + q] = r2[q]; wr[24 + q] = r3[q]; }
             if constexpr (SD_SW == 48) {
+                // the first four loads are still in flight (SD_W32 is empty): the wait here covers
+                // all six, and r0..r3 are tied in so nothing reads them before it
                 u32x8 r4, r5;
-                asm volatile("s_load_dwordx8 %0, %2, 0x80\n\t"
-                             "s_load_dwordx8 %1, %2, 0xa0\n\t"
+                asm volatile("s_load_dwordx8 %0, %6, 0x80\n\t"
+                             "s_load_dwordx8 %1, %6, 0xa0\n\t"
                              "s_waitcnt lgkmcnt(0)"
-                             : "=&s"(r4), "=&s"(r5)
+                             : "=&s"(r4), "=&s"(r5), "+s"(r0), "+s"(r1), "+s"(r2), "+s"(r3)
                              : "s"(gw)
                              : "memory");
 #pragma unroll
                 for (int q = 0; q < 8; ++q) { wr[32 + q] = r4[q]; wr[40 + q] = r5[q]; }
             }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) { wr[q] = r0[q]; wr[8 + q] = r1[q]; wr[16 + q] = r2[q]; wr[24 + q] = r3[q]; }
             // whole steps of four straight from the window, no per-entry selects (an issue past
             // the last step reads a stale record's LDS slot, which no add uses)
             const int nfull = nw & ~3;
