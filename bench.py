@@ -10,6 +10,13 @@ weak-scaled by output rows: rank g computes rows [g*d, (g+1)*d) of the (N*d) x n
 operator DenseDist(N*d, m) (ro_s = g*d, the reference's reproducible-submatrix property) and an
 RCCL all-gather reassembles the full ColMajor sketch on every rank inside the timed step.
 
+SASO (c3) shards by columns instead: rank g owns columns [g*n, (g+1)*n) of an
+m x (N*n) A -- it reads only those -- samples the same operator, and the all-gather of the
+contiguous ColMajor column blocks reassembles the d x (N*n) sketch.
+
+`--gpus N` with N > 1 outside torchrun relaunches itself under `torch.distributed.run` (one rank per
+GPU, 127.0.0.1 rendezvous) before anything touches the GPU; under torchrun WORLD_SIZE must equal N.
+
 Prints ONE JSON line (rank 0). value = N*d*n / t_step (entries/s, whole job); roofline = the fused
 GEMM kernel's algorithmic flops (2*d*m*n per launch) / its average launch time measured with HIP
 events on the launch stream; cpu_baseline = the oracle's OpenMP fill + host BLAS dgemm (the
@@ -38,6 +45,7 @@ HBM_PEAK = 8.0e12
 
 CONFIGS = {
     # name: (kind, dtype, d, m, n, vec_nnz)
+    "c1": ("dense", "f64", 128, 4096, 4096, 0),      # configs[0]: the reference's CPU plumbing case
     "c2": ("dense", "f64", 1024, 16384, 16384, 0),
     "ns": ("dense", "f64", 2048, 16384, 16384, 0),
     "c3": ("saso", "f64", 1024, 16384, 16384, 8),
@@ -112,6 +120,39 @@ def cpu_baseline(kind, dtype, d, m, n, vec_nnz, target_s=10.0):
     }
 
 
+def relaunch(ngpus: int) -> int:
+    """Run this same command as `ngpus` ranks under torch.distributed.run (a child process; this
+    process has not touched the GPU) and return its exit code."""
+    import socket
+    import subprocess
+
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ngpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"bench: launching {ngpus} ranks: {' '.join(cmd)}")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def dry_run(args, world, rank):
+    """--dry-run: the launch / rendezvous / reporting path without device work (CPU, gloo):
+    every rank joins, the max-over-ranks reduction runs, rank 0 prints the line's skeleton."""
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.tensor([float(rank)], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_max": float(t.item()), "config": args.config,
+                          "steps": args.steps, "warmup": args.warmup}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     faulthandler.enable()
     ap = argparse.ArgumentParser()
@@ -121,11 +162,20 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--chunks", type=int, default=4, help="column chunks pipelined with the all-gather (N > 1)")
+    ap.add_argument("--dry-run", action="store_true", help="launch/report path only, no device work (CPU, gloo)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(relaunch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}")
+        sys.exit(2)
+    if args.dry_run:
+        dry_run(args, world, rank)
+        return
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -136,37 +186,57 @@ def main():
     tdt = torch.float64 if dtype == "f64" else torch.float32
     stream = torch.cuda.current_stream(dev)
 
-    # A ~ DenseDist(m, n) Gaussian key 99, ColMajor, generated on the device (input, not timed)
+    # A ~ DenseDist(m, n) Gaussian key 99, ColMajor, generated on the device (input, not timed).
+    # SASO shards by columns: rank g holds columns [g n, (g+1) n) of DenseDist(m, world n).
     A = torch.empty(m * n, dtype=tdt, device=dev)
-    rb.fill_dense("C", rb.DenseDist(m, n), m, n, 0, 0, A, rb.RNGState(99))
     if kind == "saso":
-        S = rb.SparseSkOp(rb.SparseDist(world * d, m, vec_nnz), rb.RNGState(0))
+        rb.fill_dense("C", rb.DenseDist(m, world * n), m, n, 0, rank * n, A, rb.RNGState(99))
+        S = rb.SparseSkOp(rb.SparseDist(d, m, vec_nnz), rb.RNGState(0))
     else:
+        rb.fill_dense("C", rb.DenseDist(m, n), m, n, 0, 0, A, rb.RNGState(99))
         S = rb.DenseSkOp(rb.DenseDist(world * d, m), rb.RNGState(0))
     if kind == "sksy":   # A symmetric: A := (A + A^T) / 2 (input prep, not timed)
         Am = A.view(n, m)
         A.copy_(((Am + Am.t()) * 0.5).reshape(-1))
+        del Am
 
     k_ev = []   # (start, end) HIP events around every library call of the timed steps
 
+    def timed(fn, record):
+        if not record:
+            fn()
+            return
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        fn()
+        e1.record(stream)
+        k_ev.append((e0, e1))
+
     def compute(ro_s, j0, j1, out, record=False):
-        """This rank's shard B[ro_s : ro_s + d, j0 : j1] = S[ro_s : ro_s + d, :] * A[:, j0 : j1]."""
-        e0 = e1 = None
-        if record:
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
+        """This rank's shard of B = S A over columns j0 .. j1 of its A: rows ro_s .. ro_s + d (dense),
+        all d rows (SASO, whose A block is already this rank's columns)."""
         Ach = A[j0 * m:]
-        if kind == "sksy":
-            rb.sketch_symmetric_left("C", d, j1 - j0, 1.0, S, Ach, m, 0.0, out, d, ro_s=ro_s, sym_check_tol=-1.0)
-        else:
-            rb.sketch_general_left("C", "N", "N", d, j1 - j0, m, 1.0, S, Ach, m, 0.0, out, d, ro_s=ro_s)
-        if record:
-            e1.record(stream)
-            k_ev.append((e0, e1))
+        timed(lambda: rb.sketch_general_left("C", "N", "N", d, j1 - j0, m, 1.0, S, Ach, m, 0.0, out, d, ro_s=ro_s),
+              record)
+
+    def symcheck(record=False):
+        # sketch_symmetric's util::require_symmetric with the reference's default tol = 0
+        # (sksy.hh:520-537, util.hh:165-188): part of every C5 step, timed with it
+        timed(lambda: rb.require_symmetric("C", A, n, n, 0.0), record)
 
     recording = [False]
-    if world > 1:
+    if world > 1 and kind == "saso":
+        from randblas_amd.distributed import ColumnShardedSketch
+
+        B_full = torch.empty(d * world * n, dtype=tdt, device=dev)
+        drv = ColumnShardedSketch(d, n, lambda j0, j1, out: compute(0, j0, j1, out, recording[0]), tdt, dev,
+                                  chunks=args.chunks)
+
+        def step(record=False):
+            recording[0] = record
+            drv(B_full)
+    elif world > 1:
         from randblas_amd.distributed import RowShardedSketch
 
         B_full = torch.empty(world * d * n, dtype=tdt, device=dev)
@@ -175,11 +245,15 @@ def main():
 
         def step(record=False):
             recording[0] = record
+            if kind == "sksy":
+                symcheck(record)
             drv(B_full)
     else:
         B = torch.empty(d * n, dtype=tdt, device=dev)
 
         def step(record=False):
+            if kind == "sksy":
+                symcheck(record)
             compute(0, 0, n, B, record)
 
     for _ in range(args.warmup):
@@ -235,7 +309,7 @@ def main():
     if rank == 0:
         line = {
             "metric": "sketched-entries/sec (d*n/s) + achieved-%-of-fp64-MFMA-peak, skge d x m * m x n",
-            "value": world * d * n / (ms_step * 1e-3),
+            "value": world * d * n / (ms_step * 1e-3),   # d x (world n) entries for SASO, (world d) x n dense
             "unit": "sketched entries/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -249,14 +323,18 @@ def main():
             "vs_baseline": None,
             "dtype": dtype,
             "data": "synthetic (A ~ Gaussian DenseDist(m,n) key 99 generated on device; S regenerated in-kernel)",
-            "config": {"workload": {"c2": "Gaussian skge fp64 (BASELINE configs[1])",
+            "config": {"workload": {"c1": "Gaussian skge fp64 d=128 A 4096^2 (BASELINE configs[0], the reference's CPU case)",
+                                    "c2": "Gaussian skge fp64 (BASELINE configs[1])",
                                     "ns": "Gaussian skge fp64 north-star",
                                     "c3": "SASO SparseSkOp vec_nnz=8 fp64 (configs[2])",
                                     "c4": "Gaussian skge fp32 (configs[3])",
                                     "c5": "sksy fp64 (configs[4])"}[args.config],
-                       "d": world * d, "d_per_gpu": d, "m": m, "n": n, "layout": "ColMajor",
+                       "d": d if kind == "saso" else world * d, "d_per_gpu": d, "m": m,
+                       "n": world * n if kind == "saso" else n, "n_per_gpu": n, "layout": "ColMajor",
                        "operator": "SparseSkOp SASO" if kind == "saso" else "DenseSkOp Gaussian MajorAxis::Long",
-                       "parallelism": f"row-shard x{world} + RCCL all-gather" if world > 1 else "single GPU"},
+                       "symmetry_check": "tol=0 (timed in the step)" if kind == "sksy" else None,
+                       "parallelism": (f"{'column' if kind == 'saso' else 'row'}-shard x{world} + RCCL all-gather"
+                                       if world > 1 else "single GPU")},
             "pct_of_peak": roof["frac"] * 100.0,
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -25,7 +25,9 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <tuple>
 #include <type_traits>
+#include <vector>
 
 #include "randblas_hip.h"
 
@@ -374,6 +376,47 @@ void fill_sparse(SparseSkOpT &S) {
     S.known_filled = true;
 }
 
+namespace sparse_data {
+enum class NonzeroSort : char { CSC = 'C', CSR = 'R', None = 'N' };   // coo_matrix.hh:48-52
+}  // namespace sparse_data
+
+namespace detail {
+// coo_sort_type (coo_matrix.hh:76-101) of the view whose (row, col) of entry e is (r[e], c[e])
+template <typename sint_t>
+sparse_data::NonzeroSort coo_sort_type(int64_t nnz, const sint_t *r, const sint_t *c) {
+    bool csc = true, csr = true;
+    for (int64_t e = 1; e < nnz && (csc || csr); ++e) {
+        if (csc) csc = c[e - 1] < c[e] || (c[e - 1] == c[e] && r[e - 1] <= r[e]);
+        if (csr) csr = r[e - 1] < r[e] || (r[e - 1] == r[e] && c[e - 1] <= c[e]);
+    }
+    return csc ? sparse_data::NonzeroSort::CSC : (csr ? sparse_data::NonzeroSort::CSR : sparse_data::NonzeroSort::None);
+}
+
+// The state the reference's COO apply leaves the caller's arrays in. apply_coo_left_jki_p11
+// (coo_spmm_impl.hh:98-103) sorts them in place into CSC order of the view it applies, then
+// "restores" the original order with sort_coo_data (coo_matrix.hh:267-318), which does nothing for
+// NonzeroSort::None: arrays that were neither CSC- nor CSR-sorted stay CSC-sorted (by the view's
+// column, then row); CSC- or CSR-sorted arrays end as they began. Host arrays only: device
+// arrays are the caller's to keep (the reference has none).
+template <typename T, typename sint_t>
+void coo_sort_as_reference(int64_t nnz, sint_t *rows, sint_t *cols, T *vals, bool view_transposed) {
+    if (nnz < 2 || !rows || !cols || !vals || rbh_is_device_pointer(rows)) return;
+    sint_t *vr = view_transposed ? cols : rows, *vc = view_transposed ? rows : cols;
+    if (coo_sort_type(nnz, vr, vc) != sparse_data::NonzeroSort::None) return;
+    std::vector<std::tuple<sint_t, sint_t, T>> t;
+    t.reserve((size_t)nnz);
+    for (int64_t e = 0; e < nnz; ++e) t.emplace_back(vc[e], vr[e], vals[e]);
+    std::sort(t.begin(), t.end(), [](const auto &a, const auto &b) {
+        return std::get<0>(a) < std::get<0>(b) || (std::get<0>(a) == std::get<0>(b) && std::get<1>(a) < std::get<1>(b));
+    });
+    for (int64_t e = 0; e < nnz; ++e) {
+        vc[e] = std::get<0>(t[e]);
+        vr[e] = std::get<1>(t[e]);
+        vals[e] = std::get<2>(t[e]);
+    }
+}
+}  // namespace detail
+
 // ---------------------------------------------------------------------------------------------
 // sketch_general (skge.hh:771-1214)
 // ---------------------------------------------------------------------------------------------
@@ -386,16 +429,24 @@ void lsk(blas::Layout layout, blas::Op opS, blas::Op opA, int64_t d, int64_t n, 
     check(Api<T>::lskge3((char)layout, (char)opS, (char)opA, d, n, m, alpha, &dd, &s, S.buff, (char)S.layout, ro_s,
                          co_s, A, lda, beta, B, ldb, nullptr));
 }
+// sparse::lskges / rskges begin with `if (!S.known_filled) fill_sparse(S)` (skge.hh:503-504,
+// :634-635): the caller's operator comes back sampled. When this call did the sampling, the
+// arrays hold exactly the device sampler's output, so the apply samples on the device again
+// (no host-to-device copy of the COO arrays); an operator that arrived filled is applied from
+// its arrays. Afterwards the arrays are permuted as the reference's COO apply leaves them.
 template <typename T, typename RNG, typename sint_t>
 void lsk(blas::Layout layout, blas::Op opS, blas::Op opA, int64_t d, int64_t n, int64_t m, T alpha,
          SparseSkOp<T, RNG, sint_t> &S, int64_t ro_s, int64_t co_s, const T *A, int64_t lda, T beta, T *B,
          int64_t ldb) {
     const rbh_sparse_dist dd = c_dist(S.dist);
     const rbh_state s = c_state(S.seed_state);
-    const bool have = S.known_filled;
-    check(Api<T>::lskges((char)layout, (char)opS, (char)opA, d, n, m, alpha, &dd, &s, have ? S.nnz_count() : 0,
-                         have ? S.rows : nullptr, have ? S.cols : nullptr, have ? S.vals : nullptr, ro_s, co_s, A,
+    const bool given = S.known_filled;
+    if (!given) fill_sparse(S);
+    check(Api<T>::lskges((char)layout, (char)opS, (char)opA, d, n, m, alpha, &dd, &s, given ? S.nnz_count() : 0,
+                         given ? S.rows : nullptr, given ? S.cols : nullptr, given ? S.vals : nullptr, ro_s, co_s, A,
                          lda, beta, B, ldb, nullptr));
+    // left_spmm views S transposed when opS == Trans (spmm_dispatch.hh:69-87)
+    coo_sort_as_reference(S.nnz_count(), S.rows, S.cols, S.vals, opS == blas::Op::Trans);
 }
 template <typename T, typename RNG>
 void rsk(blas::Layout layout, blas::Op opA, blas::Op opS, int64_t m, int64_t d, int64_t n, T alpha, const T *A,
@@ -410,10 +461,13 @@ void rsk(blas::Layout layout, blas::Op opA, blas::Op opS, int64_t m, int64_t d, 
          int64_t lda, SparseSkOp<T, RNG, sint_t> &S, int64_t ro_s, int64_t co_s, T beta, T *B, int64_t ldb) {
     const rbh_sparse_dist dd = c_dist(S.dist);
     const rbh_state s = c_state(S.seed_state);
-    const bool have = S.known_filled;
+    const bool given = S.known_filled;
+    if (!given) fill_sparse(S);
     check(Api<T>::rskges((char)layout, (char)opA, (char)opS, m, d, n, alpha, A, lda, &dd, &s,
-                         have ? S.nnz_count() : 0, have ? S.rows : nullptr, have ? S.cols : nullptr,
-                         have ? S.vals : nullptr, ro_s, co_s, beta, B, ldb, nullptr));
+                         given ? S.nnz_count() : 0, given ? S.rows : nullptr, given ? S.cols : nullptr,
+                         given ? S.vals : nullptr, ro_s, co_s, beta, B, ldb, nullptr));
+    // right_spmm calls left_spmm with opS flipped (spmm_dispatch.hh:194-199): transposed view iff NoTrans
+    coo_sort_as_reference(S.nnz_count(), S.rows, S.cols, S.vals, opS == blas::Op::NoTrans);
 }
 }  // namespace detail
 
@@ -540,10 +594,13 @@ struct COOMatrix {
     IndexBase index_base = IndexBase::Zero;
     T *vals = nullptr;
     sint_t *rows = nullptr, *cols = nullptr;
+    NonzeroSort sort = NonzeroSort::None;   // coo_matrix.hh:125
     COOMatrix(int64_t n_rows, int64_t n_cols, int64_t nnz, T *vals, sint_t *rows, sint_t *cols,
               bool compute_sort_type = true, IndexBase index_base = IndexBase::Zero)
         : n_rows(n_rows), n_cols(n_cols), own_memory(false), nnz(nnz), index_base(index_base), vals(vals), rows(rows),
-          cols(cols) { (void)compute_sort_type; }
+          cols(cols) {
+        if (compute_sort_type && !rbh_is_device_pointer(rows)) sort = detail::coo_sort_type(nnz, rows, cols);
+    }
     COOMatrix(int64_t n_rows, int64_t n_cols) : n_rows(n_rows), n_cols(n_cols), own_memory(true) {}
     void reserve(int64_t n) {
         RBH_CXX_REQUIRE(own_memory && vals == nullptr);
@@ -610,6 +667,30 @@ using sparse_data::COOMatrix;
 using sparse_data::CSCMatrix;
 using sparse_data::CSRMatrix;
 
+namespace detail {
+template <typename SpMat, typename = void> struct is_spmat : std::false_type {};
+template <typename SpMat>
+struct is_spmat<SpMat, std::void_t<decltype(SpMat::fmt), decltype(std::declval<SpMat &>().idx_arr())>>
+    : std::true_type {};
+template <typename T> struct SpmmApi;
+template <> struct SpmmApi<double> {
+    static constexpr auto left = rbh_spmm_left_f64;
+    static constexpr auto right = rbh_spmm_right_f64;
+};
+template <> struct SpmmApi<float> {
+    static constexpr auto left = rbh_spmm_left_f32;
+    static constexpr auto right = rbh_spmm_right_f32;
+};
+// a COOMatrix's arrays after the reference's COO apply of a view (transposed or not) of it
+template <typename SpMat>
+void coo_after_apply(SpMat &A, bool view_transposed) {
+    if constexpr (SpMat::fmt == 'O') {
+        coo_sort_as_reference(A.nnz, A.rows, A.cols, A.vals, view_transposed);
+        if (!rbh_is_device_pointer(A.rows)) A.sort = coo_sort_type(A.nnz, A.rows, A.cols);
+    }
+}
+}  // namespace detail
+
 // B = alpha op(submat(S)) op(submat(A)) + beta B, A sparse (sksp.hh:464-485 -> lsksp3, :147-192)
 template <typename T, typename SpMat, typename RNG>
 inline void sketch_sparse(blas::Layout layout, blas::Op opS, blas::Op opA, int64_t d, int64_t n, int64_t m, T alpha,
@@ -622,6 +703,7 @@ inline void sketch_sparse(blas::Layout layout, blas::Op opS, blas::Op opA, int64
                                          (char)S.layout, ro_s, co_s, SpMat::fmt, A.n_rows, A.n_cols, A.nnz,
                                          (const int64_t *)A.ptr_arr(), (const int64_t *)A.idx_arr(), A.vals, ro_a,
                                          co_a, beta, B, ldb, nullptr));
+    detail::coo_after_apply(A, opA == blas::Op::NoTrans);   // lsksp3 -> right_spmm flips opA (sksp.hh:190)
 }
 
 // B = alpha op(submat(A)) op(submat(S)) + beta B, A sparse (sksp.hh:595-615 -> rsksp3, :302-350)
@@ -636,6 +718,32 @@ inline void sketch_sparse(blas::Layout layout, blas::Op opA, blas::Op opS, int64
                                          A.n_cols, A.nnz, (const int64_t *)A.ptr_arr(), (const int64_t *)A.idx_arr(),
                                          A.vals, ro_a, co_a, &dd, &s, S.buff, (char)S.layout, ro_s, co_s, beta, B,
                                          ldb, nullptr));
+    detail::coo_after_apply(A, opA == blas::Op::Trans);   // rsksp3 -> left_spmm(opA) (sksp.hh:343)
+}
+
+// ---------------------------------------------------------------------------------------------
+// RandBLAS::spmm (sparse_data/spmm_dispatch.hh:290-294, :380-384)
+// ---------------------------------------------------------------------------------------------
+// C = alpha * op(submat(A)) * op(B) + beta * C, A sparse (m x k after op), B dense
+template <typename T, typename SpMat, std::enable_if_t<detail::is_spmat<SpMat>::value, int> = 0>
+inline void spmm(blas::Layout layout, blas::Op opA, blas::Op opB, int64_t m, int64_t n, int64_t k, T alpha, SpMat &A,
+                 int64_t ro_a, int64_t co_a, const T *B, int64_t ldb, T beta, T *C, int64_t ldc) {
+    RBH_CXX_REQUIRE(A.index_base == sparse_data::IndexBase::Zero);
+    detail::check(detail::SpmmApi<T>::left((char)layout, (char)opA, (char)opB, m, n, k, alpha, SpMat::fmt, A.n_rows,
+                                           A.n_cols, A.nnz, (const int64_t *)A.ptr_arr(), (const int64_t *)A.idx_arr(),
+                                           A.vals, ro_a, co_a, B, ldb, beta, C, ldc, nullptr));
+    detail::coo_after_apply(A, opA == blas::Op::Trans);
+}
+
+// C = alpha * op(A) * op(submat(B)) + beta * C, A dense (m x k after op), B sparse
+template <typename T, typename SpMat, std::enable_if_t<detail::is_spmat<SpMat>::value, int> = 0>
+inline void spmm(blas::Layout layout, blas::Op opA, blas::Op opB, int64_t m, int64_t n, int64_t k, T alpha, const T *A,
+                 int64_t lda, SpMat &B, int64_t ro_b, int64_t co_b, T beta, T *C, int64_t ldc) {
+    RBH_CXX_REQUIRE(B.index_base == sparse_data::IndexBase::Zero);
+    detail::check(detail::SpmmApi<T>::right((char)layout, (char)opA, (char)opB, m, n, k, alpha, A, lda, SpMat::fmt,
+                                            B.n_rows, B.n_cols, B.nnz, (const int64_t *)B.ptr_arr(),
+                                            (const int64_t *)B.idx_arr(), B.vals, ro_b, co_b, beta, C, ldc, nullptr));
+    detail::coo_after_apply(B, opB == blas::Op::NoTrans);   // right_spmm flips opB (:194)
 }
 
 }  // namespace RandBLAS

@@ -55,6 +55,9 @@ typedef struct rbh_sparse_dist {
 
 int rbh_abi_version(void);
 const char *rbh_last_error(void);
+/* 1 if p is device (or managed) memory, 0 for host memory (hipPointerGetAttributes). The drop-in
+ * header uses it to keep host-only reference behaviour (in-place COO sorting) off device arrays. */
+int rbh_is_device_pointer(const void *p);
 
 /* Diagnostics (no reference counterpart): HIP-event timing of the dominant kernel of every call
  * (the fused GEMM, the sparse apply), recorded on the call's stream while enabled. collect()
@@ -173,6 +176,32 @@ int rbh_rsksp3_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_
                    const float *A_v, int64_t ro_a, int64_t co_a, const rbh_dense_dist *D, const rbh_state *seed,
                    const float *S_buff, char S_layout, int64_t ro_s, int64_t co_s, float beta, float *B, int64_t ldb,
                    void *stream);
+
+/* RandBLAS::spmm with the sparse matrix on the left (sparse_data/spmm_dispatch.hh:290-294 ->
+ * left_spmm, :48-160): C = alpha * op(submat(A)) * op(B) + beta * C, C m x n, op(submat(A)) m x k
+ * at (ro_a, co_a) of the sparse A (format as for sketch_sparse), B dense. The argument checks
+ * are left_spmm's (:69-132): a COO window must fit inside A; CSR / CSC must match m x k exactly
+ * with zero offsets. Entries of C accumulate in ascending contracted index. */
+int rbh_spmm_left_f64(char layout, char opA, char opB, int64_t m, int64_t n, int64_t k, double alpha, char A_fmt,
+                      int64_t A_rows, int64_t A_cols, int64_t A_nnz, const int64_t *A_p, const int64_t *A_i,
+                      const double *A_v, int64_t ro_a, int64_t co_a, const double *B, int64_t ldb, double beta,
+                      double *C, int64_t ldc, void *stream);
+int rbh_spmm_left_f32(char layout, char opA, char opB, int64_t m, int64_t n, int64_t k, float alpha, char A_fmt,
+                      int64_t A_rows, int64_t A_cols, int64_t A_nnz, const int64_t *A_p, const int64_t *A_i,
+                      const float *A_v, int64_t ro_a, int64_t co_a, const float *B, int64_t ldb, float beta, float *C,
+                      int64_t ldc, void *stream);
+/* RandBLAS::spmm with the sparse matrix on the right (spmm_dispatch.hh:380-384 -> right_spmm,
+ * :162-200): C = alpha * op(A) * op(submat(B)) + beta * C, C m x n, op(A) m x k dense, op(submat(B))
+ * k x n at (ro_b, co_b) of the sparse B. (The reference's own overload passes B twice, :382, and
+ * does not compile when instantiated; this entry point does what right_spmm specifies.) */
+int rbh_spmm_right_f64(char layout, char opA, char opB, int64_t m, int64_t n, int64_t k, double alpha,
+                       const double *A, int64_t lda, char B_fmt, int64_t B_rows, int64_t B_cols, int64_t B_nnz,
+                       const int64_t *B_p, const int64_t *B_i, const double *B_v, int64_t ro_b, int64_t co_b,
+                       double beta, double *C, int64_t ldc, void *stream);
+int rbh_spmm_right_f32(char layout, char opA, char opB, int64_t m, int64_t n, int64_t k, float alpha, const float *A,
+                       int64_t lda, char B_fmt, int64_t B_rows, int64_t B_cols, int64_t B_nnz, const int64_t *B_p,
+                       const int64_t *B_i, const float *B_v, int64_t ro_b, int64_t co_b, float beta, float *C,
+                       int64_t ldc, void *stream);
 
 /* ---- sketch_symmetric support ------------------------------------------------------------- */
 /* util::require_symmetric (util.hh:165-188) on the device: RBH_OK if |A_ij - A_ji| <=

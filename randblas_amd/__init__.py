@@ -103,6 +103,11 @@ for _t, _ct in (("f64", ctypes.c_double), ("f32", ctypes.c_float)):
         [_ct, c_vp, c_i64, c_vp]
     getattr(lib, f"rbh_rsksp3_{_t}").argtypes = [c_char, c_char, c_char, c_i64, c_i64, c_i64, _ct] + _spm + _dop + \
         [_ct, c_vp, c_i64, c_vp]
+    getattr(lib, f"rbh_spmm_left_{_t}").argtypes = [c_char, c_char, c_char, c_i64, c_i64, c_i64, _ct] + _spm + \
+        [c_vp, c_i64, _ct, c_vp, c_i64, c_vp]
+    getattr(lib, f"rbh_spmm_right_{_t}").argtypes = [c_char, c_char, c_char, c_i64, c_i64, c_i64, _ct, c_vp, c_i64] + \
+        _spm + [_ct, c_vp, c_i64, c_vp]
+lib.rbh_is_device_pointer.argtypes = [c_vp]
 
 # --------------------------------------------------------------------------------------------
 # Python mirror of the reference's types
@@ -455,6 +460,26 @@ def sketch_sparse(layout, op1, op2, d_or_m, n_or_d, m_or_n, alpha, X, Y, *args, 
     return sketch_sparse_right(layout, op1, op2, d_or_m, n_or_d, m_or_n, alpha, X, Y, *args, **kw)
 
 
+def spmm(layout, opA, opB, m, n, k, alpha, X, x_off_r, x_off_c_or_ld, Y, *args, stream=None):
+    """RandBLAS::spmm (sparse_data/spmm_dispatch.hh:290-294 and :380-384), both overloads:
+      spmm(layout, opA, opB, m, n, k, alpha, A_sparse, ro_a, co_a, B, ldb, beta, C, ldc)
+      spmm(layout, opA, opB, m, n, k, alpha, A, lda, B_sparse, ro_b, co_b, beta, C, ldc)
+    C (m x n) = alpha * op(A) * op(B) + beta * C with one sparse factor (COO / CSR / CSC)."""
+    if isinstance(X, (COOMatrix, CSRMatrix, CSCMatrix)):
+        ro_a, co_a, B = x_off_r, x_off_c_or_ld, Y
+        ldb, beta, C, ldc = args
+        t = _dtype_tag(C)
+        _check(getattr(lib, f"rbh_spmm_left_{t}")(_b(layout), _b(opA), _b(opB), m, n, k, alpha, *_spm_args(X), ro_a,
+                                                   co_a, _ptr(B), ldb, beta, _ptr(C), ldc, _stream(C, stream)))
+    else:
+        A, lda, Bs = X, x_off_r, x_off_c_or_ld
+        ro_b, co_b, beta, C, ldc = (Y,) + tuple(args)
+        t = _dtype_tag(C)
+        _check(getattr(lib, f"rbh_spmm_right_{t}")(_b(layout), _b(opA), _b(opB), m, n, k, alpha, _ptr(A), lda,
+                                                    *_spm_args(Bs), ro_b, co_b, beta, _ptr(C), ldc,
+                                                    _stream(C, stream)))
+
+
 def kernel_timing(on: bool) -> None:
     """Enable/disable HIP-event timing of each call's dominant kernel (diagnostics)."""
     lib.rbh_kernel_timing_enable(1 if on else 0)
@@ -476,5 +501,5 @@ __all__ = [
     "sketch_general", "sketch_general_left", "sketch_general_right", "sketch_symmetric_left",
     "sketch_symmetric_right", "require_symmetric", "dense_next_state", "sparse_next_state", "abi_version", "lib",
     "LIB_PATH", "kernel_timing", "kernel_times_ms", "sketch_vector", "sketch_vector_full", "COOMatrix",
-    "CSRMatrix", "CSCMatrix", "sketch_sparse", "sketch_sparse_left", "sketch_sparse_right",
+    "CSRMatrix", "CSCMatrix", "sketch_sparse", "sketch_sparse_left", "sketch_sparse_right", "spmm",
 ]

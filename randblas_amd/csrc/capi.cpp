@@ -9,7 +9,7 @@
 // works unchanged; device arrays are used in place and the work is stream-ordered.
 #include <hip/hip_runtime.h>
 
-#include <atomic>
+#include <mutex>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -54,6 +54,39 @@ void timing_end(hipStream_t s) {
     g_timing.pending = nullptr;
     g_timing.used++;
 }
+
+// Workspaces: one stream-ordered pool per device, created on first use and private to this
+// library. It keeps up to RBH_POOL_KEEP_BYTES (default 1 GiB) of freed memory across
+// synchronisations, so repeated calls reuse their workspaces instead of remapping them.
+namespace {
+std::mutex g_pool_mu;
+hipMemPool_t g_pool[64] = {};
+}  // namespace
+hipError_t ws_alloc(void **p, size_t bytes, hipStream_t s) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    hipMemPool_t pool;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        if (!g_pool[dev]) {
+            hipMemPoolProps props{};
+            props.allocType = hipMemAllocationTypePinned;
+            props.handleTypes = hipMemHandleTypeNone;
+            props.location.type = hipMemLocationTypeDevice;
+            props.location.id = dev;
+            e = hipMemPoolCreate(&g_pool[dev], &props);
+            if (e != hipSuccess) { g_pool[dev] = nullptr; return e; }
+            const char *k = getenv("RBH_POOL_KEEP_BYTES");
+            uint64_t keep = k ? strtoull(k, nullptr, 10) : (1ull << 30);
+            (void)hipMemPoolSetAttribute(g_pool[dev], hipMemPoolAttrReleaseThreshold, &keep);
+        }
+        pool = g_pool[dev];
+    }
+    return hipMallocFromPoolAsync(p, bytes, pool, s);
+}
+hipError_t ws_free(void *p, hipStream_t s) { return p ? hipFreeAsync(p, s) : hipSuccess; }
 }  // namespace rbh
 
 namespace {
@@ -75,6 +108,13 @@ int set_error(int code, const char *fmt, ...) {
         if (!(cond))                                                                                       \
             return set_error(RBH_ERR_REQUIRE, "(%s) was required, but did not hold, in function %s", #cond, \
                              __func__);                                                                    \
+    } while (0)
+
+// the same, with the reference's own condition text and function name
+#define RBH_REQUIRE_AS(cond, text, func)                                                                     \
+    do {                                                                                                   \
+        if (!(cond))                                                                                       \
+            return set_error(RBH_ERR_REQUIRE, "(%s) was required, but did not hold, in function %s", text, func); \
     } while (0)
 
 #define RBH_HIP(expr)                                                                                 \
@@ -102,41 +142,38 @@ int64_t extent(char layout, int64_t rows, int64_t cols, int64_t ld) {
 }
 
 // A host or device buffer seen from the device. Host buffers get a device copy (in: copied
-// H2D; out: copied back D2H by finish()).
+// H2D; out: copied back D2H by finish()). For an output only the matrix window is copied back:
+// `runs` contiguous runs of `run` bytes, `pitch` bytes apart (a ColMajor rows x cols window with
+// leading dimension ld is cols runs of rows elements, ld elements apart). The bytes between runs
+// (ld padding, the gaps of a strided vector) are the caller's and are never written, as BLAS
+// leaves them; with beta == 0 they were never copied in either.
 struct Staged {
     void *host = nullptr;
     void *dev = nullptr;
     size_t bytes = 0;
     bool owned = false;
     bool out = false;
+    size_t run = 0, runs = 1, pitch = 0;
 };
-
-// Workspaces come from the device's default stream-ordered pool (hipMallocAsync). With the default
-// release threshold (0) the pool trims its memory at every synchronisation; in a process without
-// torch (a C/C++ client on the default stream) a trimmed-and-reallocated block was observed to
-// read back zeros after a kernel had filled it. Keep the pool's memory: threshold = max, once per
-// device.
-void keep_pool_memory() {
-    static std::atomic<uint64_t> done{0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) { (void)hipGetLastError(); return; }
-    if (done.load() & (1ull << dev)) return;
-    hipMemPool_t pool;
-    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-        uint64_t thr = UINT64_MAX;
-        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-    }
-    (void)hipGetLastError();
-    done.fetch_or(1ull << dev);
-}
 
 struct Stager {
     hipStream_t s;
     std::vector<Staged> v;
     bool any_host = false;
-    explicit Stager(hipStream_t st) : s(st) { keep_pool_memory(); }
+    explicit Stager(hipStream_t st) : s(st) {}
     // returns device pointer (or nullptr on error / null input)
     hipError_t map(const void *p, size_t bytes, bool copy_in, bool out, void **dptr) {
+        return map_window(p, bytes, copy_in, out, bytes, 1, bytes, dptr);
+    }
+    // an output matrix window (layout, rows x cols, leading dimension ld, esz-byte elements)
+    hipError_t map_out(void *p, size_t esz, char layout, int64_t rows, int64_t cols, int64_t ld, bool copy_in,
+                       void **dptr) {
+        const int64_t inner = layout == 'C' ? rows : cols, outer = layout == 'C' ? cols : rows;
+        return map_window(p, esz * (size_t)extent(layout, rows, cols, ld), copy_in, true, esz * (size_t)inner,
+                          (size_t)outer, esz * (size_t)ld, dptr);
+    }
+    hipError_t map_window(const void *p, size_t bytes, bool copy_in, bool out, size_t run, size_t runs, size_t pitch,
+                          void **dptr) {
         *dptr = nullptr;
         if (!p || bytes == 0) { *dptr = const_cast<void *>(p); return hipSuccess; }
         if (is_device_ptr(p)) { *dptr = const_cast<void *>(p); return hipSuccess; }
@@ -146,6 +183,9 @@ struct Stager {
         st.bytes = bytes;
         st.out = out;
         st.owned = true;
+        st.run = run;
+        st.runs = runs;
+        st.pitch = pitch;
         hipError_t e = hipMalloc(&st.dev, bytes);
         if (e != hipSuccess) return e;
         if (copy_in) {
@@ -165,14 +205,19 @@ struct Stager {
             hipError_t e = hipStreamSynchronize(s);
             if (e != hipSuccess) err = e;
         }
-        for (auto &st : v)
-            if (st.out) {
-                hipError_t e = hipMemcpyAsync(st.host, st.dev, st.bytes, hipMemcpyDeviceToHost, s);
-                if (e != hipSuccess && err == hipSuccess) err = e;
+        for (auto &st : v) {
+            if (!st.out || err != hipSuccess) continue;
+            if (st.runs <= 1 || st.run == st.pitch) {   // the window is the whole extent
+                hipError_t e = hipMemcpy(st.host, st.dev, st.bytes, hipMemcpyDeviceToHost);
+                if (e != hipSuccess) err = e;
+                continue;
             }
-        if (any_host) {
-            hipError_t e = hipStreamSynchronize(s);
-            if (e != hipSuccess && err == hipSuccess) err = e;
+            // padded window: bring the extent to a private host buffer, then copy the runs
+            std::vector<char> tmp(st.bytes);
+            hipError_t e = hipMemcpy(tmp.data(), st.dev, st.bytes, hipMemcpyDeviceToHost);
+            if (e != hipSuccess) { err = e; continue; }
+            for (size_t r = 0; r < st.runs; ++r)
+                memcpy((char *)st.host + r * st.pitch, tmp.data() + r * st.pitch, st.run);
         }
         for (auto &st : v)
             if (st.owned) (void)hipFree(st.dev);
@@ -278,7 +323,7 @@ int lskge3(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, T a
     Stager st(s);
     void *dA, *dB, *dS;
     RBH_HIP(st.map(A, sizeof(T) * extent(layout, rows_A, cols_A, lda), true, false, &dA));
-    RBH_HIP(st.map(B, sizeof(T) * extent(layout, d, n, ldb), beta != (T)0, true, &dB));
+    RBH_HIP(st.map_out(B, sizeof(T), layout, d, n, ldb, beta != (T)0, &dB));
     RBH_HIP(st.map(S_buff, sizeof(T) * D->n_rows * D->n_cols, true, false, &dS));
 
     GemmProblem p{};
@@ -356,7 +401,7 @@ int rskge3(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, T a
     Stager st(s);
     void *dA, *dB, *dS;
     RBH_HIP(st.map(A, sizeof(T) * extent(layout, rows_A, cols_A, lda), true, false, &dA));
-    RBH_HIP(st.map(B, sizeof(T) * extent(layout, m, d, ldb), beta != (T)0, true, &dB));
+    RBH_HIP(st.map_out(B, sizeof(T), layout, m, d, ldb, beta != (T)0, &dB));
     RBH_HIP(st.map(S_buff, sizeof(T) * D->n_rows * D->n_cols, true, false, &dS));
 
     GemmProblem p{};
@@ -558,12 +603,12 @@ int check_left_spmm(char layout, char opS, char opB, int64_t d, int64_t n, int64
 
 template <typename T>
 int sparse_common(SparseApply &p, const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz, const int64_t *rows,
-                  const int64_t *cols, const T *vals, const T *A, int64_t A_extent, T *B, int64_t B_extent,
-                  T beta, hipStream_t s) {
+                  const int64_t *cols, const T *vals, const T *A, int64_t A_extent, T *B, char layout,
+                  int64_t B_rows, int64_t B_cols, int64_t ldb, T beta, hipStream_t s) {
     Stager st(s);
     void *dA, *dB;
     RBH_HIP(st.map(A, sizeof(T) * A_extent, true, false, &dA));
-    RBH_HIP(st.map(B, sizeof(T) * B_extent, beta != (T)0, true, &dB));
+    RBH_HIP(st.map_out(B, sizeof(T), layout, B_rows, B_cols, ldb, beta != (T)0, &dB));
     p.Y = dA;
     p.C = dB;
     if (const char *ab = getenv("RBH_SASO_ABLATE")) p.ablate = atoi(ab);   // diagnostics only
@@ -609,8 +654,8 @@ int lskges(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, T a
     if (col) { p.ysk = opA == 'N' ? 1 : lda; p.ysj = opA == 'N' ? lda : 1; }
     else { p.ysk = opA == 'N' ? lda : 1; p.ysj = opA == 'N' ? 1 : lda; }
     const int64_t rows_A = opA == 'N' ? m : n, cols_A = opA == 'N' ? n : m;
-    return sparse_common<T>(p, D, seed, nnz, rows, cols, vals, A, extent(layout, rows_A, cols_A, lda), B,
-                            extent(layout, d, n, ldb), beta, (hipStream_t)stream);
+    return sparse_common<T>(p, D, seed, nnz, rows, cols, vals, A, extent(layout, rows_A, cols_A, lda), B, layout,
+                            d, n, ldb, beta, (hipStream_t)stream);
 }
 
 // right: B = alpha op(A) op(submat(S)) + beta B   (sparse::rskges, skge.hh:616-641 -> right_spmm,
@@ -644,8 +689,8 @@ int rskges(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, T a
     if (col) { p.ysk = opA == 'N' ? lda : 1; p.ysj = opA == 'N' ? 1 : lda; }
     else { p.ysk = opA == 'N' ? 1 : lda; p.ysj = opA == 'N' ? lda : 1; }
     const int64_t rows_A = opA == 'N' ? m : n, cols_A = opA == 'N' ? n : m;
-    return sparse_common<T>(p, D, seed, nnz, rows, cols, vals, A, extent(layout, rows_A, cols_A, lda), B,
-                            extent(layout, m, d, ldb), beta, (hipStream_t)stream);
+    return sparse_common<T>(p, D, seed, nnz, rows, cols, vals, A, extent(layout, rows_A, cols_A, lda), B, layout,
+                            m, d, ldb, beta, (hipStream_t)stream);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -679,7 +724,7 @@ int data_as_coo(Stager &st, char fmt, int64_t n_rows, int64_t n_cols, int64_t nn
         *cols = (const int64_t *)di;
         return RBH_OK;
     }
-    RBH_HIP(hipMallocAsync(ws, sizeof(int64_t) * nnz, s));
+    RBH_HIP(ws_alloc(ws, sizeof(int64_t) * nnz, s));
     int64_t *major = (int64_t *)*ws;
     RBH_HIP(launch_expand_ptr(fmt == 'R' ? n_rows : n_cols, (const int64_t *)dp, major, s));
     *rows = fmt == 'R' ? major : (const int64_t *)di;
@@ -706,7 +751,7 @@ int submat_dense(Stager &st, const rbh_dense_dist *D, const rbh_state *seed, con
     RBH_REQUIRE(seed != nullptr);
     RBH_REQUIRE(D->family != 'B');
     RBH_REQUIRE(D->major_axis != 'U');
-    RBH_HIP(hipMallocAsync(ws, sizeof(T) * (size_t)std::max<int64_t>(rs * cs, 1), s));
+    RBH_HIP(ws_alloc(ws, sizeof(T) * (size_t)std::max<int64_t>(rs * cs, 1), s));
     const char nat = dist_to_layout(D);
     GenOperand g{};
     memcpy(g.ctr, seed->counter, sizeof g.ctr);
@@ -743,6 +788,11 @@ int sksp3(bool left, char layout, char opS, char opA, int64_t M, int64_t N, int6
     const int64_t rows_submat_A = opA == 'N' ? aR : aC, cols_submat_A = opA == 'N' ? aC : aR;
     RBH_REQUIRE(A_rows >= rows_submat_A + ro_a);
     RBH_REQUIRE(A_cols >= cols_submat_A + co_a);
+    if (A_fmt == 'R' || A_fmt == 'C') {   // the CSR / CSC branch of left_spmm (spmm_dispatch.hh:100-103)
+        RBH_REQUIRE_AS(A_rows == rows_submat_A && A_cols == cols_submat_A, "A.n_rows == d && A.n_cols == m",
+                       "left_spmm");
+        RBH_REQUIRE_AS(ro_a == 0 && co_a == 0, "ro_a == 0 && co_a == 0", "left_spmm");
+    }
     RBH_REQUIRE(D->n_rows >= rows_submat_S + ro_s);
     RBH_REQUIRE(D->n_cols >= cols_submat_S + co_s);
     if (layout == 'C') {
@@ -753,7 +803,7 @@ int sksp3(bool left, char layout, char opS, char opA, int64_t M, int64_t N, int6
     hipStream_t s = (hipStream_t)stream;
     Stager st(s);
     void *dB;
-    RBH_HIP(st.map(B, sizeof(T) * extent(layout, M, N, ldb), beta != (T)0, true, &dB));
+    RBH_HIP(st.map_out(B, sizeof(T), layout, M, N, ldb, beta != (T)0, &dB));
     const T *Sp = nullptr;
     int64_t sr = 1, sc = 1;
     void *sws = nullptr, *aws = nullptr;
@@ -763,8 +813,8 @@ int sksp3(bool left, char layout, char opS, char opA, int64_t M, int64_t N, int6
     const T *av = nullptr;
     if (!rc) rc = data_as_coo<T>(st, A_fmt, A_rows, A_cols, A_nnz, A_p, A_i, A_v, &ar, &ac, &av, &aws, s);
     if (rc) {
-        if (sws) (void)hipFreeAsync(sws, s);
-        if (aws) (void)hipFreeAsync(aws, s);
+        if (sws) (void)ws_free(sws, s);
+        if (aws) (void)ws_free(aws, s);
         return rc;
     }
     SparseApply p{};
@@ -801,8 +851,75 @@ int sksp3(bool left, char layout, char opS, char opA, int64_t M, int64_t N, int6
     }
     const int64_t nnz = (alpha == (T)0) ? 0 : A_nnz;   // beta scaling only, as left_spmm (:134-135)
     hipError_t e = run_sparse_apply_t<T>(p, ar, ac, av, nnz, s);
-    if (sws) (void)hipFreeAsync(sws, s);
-    if (aws) (void)hipFreeAsync(aws, s);
+    if (sws) (void)ws_free(sws, s);
+    if (aws) (void)ws_free(aws, s);
+    RBH_HIP(e);
+    RBH_HIP(st.finish());
+    return RBH_OK;
+}
+
+// RandBLAS::spmm with the sparse matrix on the left (spmm_dispatch.hh:290-294 -> left_spmm, :48-160):
+//   C (d x n) = alpha * op(submat(A)) (d x m) * op(B) (m x n) + beta * C,  A sparse (COO / CSR / CSC).
+// The checks are left_spmm's, made after its opA == Trans transposition (:69-87, which swaps the
+// roles of ro_a / co_a): a COO window must fit (:97-98); CSR / CSC must match exactly with zero
+// offsets (:100-103). The product is saso.hip's ordered sparse apply with A as the operator.
+template <typename T>
+int spmm_left(char layout, char opA, char opB, int64_t d, int64_t n, int64_t m, T alpha, char A_fmt, int64_t A_rows,
+              int64_t A_cols, int64_t A_nnz, const int64_t *A_p, const int64_t *A_i, const T *A_v, int64_t ro_a,
+              int64_t co_a, const T *B, int64_t ldb, T beta, T *C, int64_t ldc, void *stream) {
+    RBH_REQUIRE(layout == 'C' || layout == 'R');
+    RBH_REQUIRE(opA == 'N' || opA == 'T');
+    RBH_REQUIRE(opB == 'N' || opB == 'T');
+    RBH_REQUIRE(A_fmt == 'O' || A_fmt == 'R' || A_fmt == 'C');
+    RBH_REQUIRE(d >= 0 && n >= 0 && m >= 0 && ro_a >= 0 && co_a >= 0);
+    {   // left_spmm's requirements on op(A) (transposed view: rows <-> cols, ro <-> co)
+        const int64_t tr = opA == 'N' ? A_rows : A_cols, tc = opA == 'N' ? A_cols : A_rows;
+        const int64_t tro = opA == 'N' ? ro_a : co_a, tco = opA == 'N' ? co_a : ro_a;
+        if (A_fmt == 'O') {
+            RBH_REQUIRE_AS(tr >= d, "A.n_rows >= d", "left_spmm");
+            RBH_REQUIRE_AS(tc >= m, "A.n_cols >= m", "left_spmm");
+        } else {
+            RBH_REQUIRE_AS(tr == d, "A.n_rows == d", "left_spmm");
+            RBH_REQUIRE_AS(tc == m, "A.n_cols == m", "left_spmm");
+            RBH_REQUIRE_AS(tro == 0, "ro_a == 0", "left_spmm");
+            RBH_REQUIRE_AS(tco == 0, "co_a == 0", "left_spmm");
+        }
+    }
+    const int64_t rows_B = opB == 'N' ? m : n, cols_B = opB == 'N' ? n : m;
+    if (layout == 'C') {
+        RBH_REQUIRE_AS(ldb >= rows_B, "ldb >= rows_B", "left_spmm");
+        RBH_REQUIRE_AS(ldc >= d, "ldc >= d", "left_spmm");
+    } else {
+        RBH_REQUIRE_AS(ldc >= n, "ldc >= n", "left_spmm");
+        RBH_REQUIRE_AS(ldb >= cols_B, "ldb >= cols_B", "left_spmm");
+    }
+    hipStream_t s = (hipStream_t)stream;
+    Stager st(s);
+    void *dB, *dC;
+    RBH_HIP(st.map(B, sizeof(T) * extent(layout, rows_B, cols_B, ldb), true, false, &dB));
+    RBH_HIP(st.map_out(C, sizeof(T), layout, d, n, ldc, beta != (T)0, &dC));
+    const int64_t *ar = nullptr, *ac = nullptr;
+    const T *av = nullptr;
+    void *aws = nullptr;
+    const int64_t nnz = alpha == (T)0 ? 0 : A_nnz;   // beta scaling only (:134-135)
+    int rc = data_as_coo<T>(st, A_fmt, A_rows, A_cols, nnz, A_p, A_i, A_v, &ar, &ac, &av, &aws, s);
+    if (rc) return rc;
+    SparseApply p{};
+    p.M = d; p.N = n; p.K = m;
+    p.alpha = alpha; p.beta = beta;
+    p.ro = ro_a; p.co = co_a;
+    p.transposed = opA == 'T';
+    p.win_r = opA == 'N' ? d : m;
+    p.win_c = opA == 'N' ? m : d;
+    p.Y = dB;
+    p.C = dC;
+    const bool col = layout == 'C';
+    p.crs = col ? 1 : ldc;
+    p.ccs = col ? ldc : 1;
+    if (col) { p.ysk = opB == 'N' ? 1 : ldb; p.ysj = opB == 'N' ? ldb : 1; }
+    else { p.ysk = opB == 'N' ? ldb : 1; p.ysj = opB == 'N' ? 1 : ldb; }
+    hipError_t e = run_sparse_apply_t<T>(p, ar, ac, av, nnz, s);
+    if (aws) (void)ws_free(aws, s);
     RBH_HIP(e);
     RBH_HIP(st.finish());
     return RBH_OK;
@@ -826,12 +943,12 @@ int require_symmetric(char layout, const T *A, int64_t n, int64_t lda, T tol, vo
     void *dA;
     RBH_HIP(st.map(A, sizeof(T) * extent(layout, n, n, lda), true, false, &dA));
     int *flag = nullptr;
-    RBH_HIP(hipMallocAsync((void **)&flag, sizeof(int), s));
+    RBH_HIP(ws_alloc((void **)&flag, sizeof(int), s));
     RBH_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
     RBH_HIP(launch_sym_t<T>(layout, (const T *)dA, n, lda, tol, flag, s));
     int h = 0;
     RBH_HIP(hipMemcpyAsync(&h, flag, sizeof(int), hipMemcpyDeviceToHost, s));
-    RBH_HIP(hipFreeAsync(flag, s));
+    RBH_HIP(ws_free(flag, s));
     RBH_HIP(hipStreamSynchronize(s));
     RBH_HIP(st.finish());
     if (h) return set_error(RBH_ERR_SYMMETRY, "Symmetry check failed, in function require_symmetric");
@@ -864,6 +981,7 @@ int rbh_kernel_timing_collect(float *ms, int max) {
     return n;
 }
 const char *rbh_last_error(void) { return g_last_error.c_str(); }
+int rbh_is_device_pointer(const void *p) { return is_device_ptr(p) ? 1 : 0; }
 
 int rbh_dense_next_state(const rbh_dense_dist *D, const rbh_state *seed, rbh_state *next) {
     RBH_REQUIRE(D && seed && next);
@@ -986,6 +1104,41 @@ int rbh_rskges_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_
                    int64_t ldb, void *stream) {
     return rskges<float>(layout, opA, opS, m, d, n, alpha, A, lda, D, seed, nnz, rows, cols, vals, ro_s, co_s, beta,
                          B, ldb, stream);
+}
+
+int rbh_spmm_left_f64(char layout, char opA, char opB, int64_t m, int64_t n, int64_t k, double alpha, char A_fmt,
+                      int64_t A_rows, int64_t A_cols, int64_t A_nnz, const int64_t *A_p, const int64_t *A_i,
+                      const double *A_v, int64_t ro_a, int64_t co_a, const double *B, int64_t ldb, double beta,
+                      double *C, int64_t ldc, void *stream) {
+    return spmm_left<double>(layout, opA, opB, m, n, k, alpha, A_fmt, A_rows, A_cols, A_nnz, A_p, A_i, A_v, ro_a,
+                             co_a, B, ldb, beta, C, ldc, stream);
+}
+int rbh_spmm_left_f32(char layout, char opA, char opB, int64_t m, int64_t n, int64_t k, float alpha, char A_fmt,
+                      int64_t A_rows, int64_t A_cols, int64_t A_nnz, const int64_t *A_p, const int64_t *A_i,
+                      const float *A_v, int64_t ro_a, int64_t co_a, const float *B, int64_t ldb, float beta, float *C,
+                      int64_t ldc, void *stream) {
+    return spmm_left<float>(layout, opA, opB, m, n, k, alpha, A_fmt, A_rows, A_cols, A_nnz, A_p, A_i, A_v, ro_a,
+                            co_a, B, ldb, beta, C, ldc, stream);
+}
+// right_spmm (spmm_dispatch.hh:162-200): C^T = op(submat(B))^T op(A)^T, i.e. left_spmm in the other
+// layout with opB flipped.
+int rbh_spmm_right_f64(char layout, char opA, char opB, int64_t m, int64_t n, int64_t k, double alpha,
+                       const double *A, int64_t lda, char B_fmt, int64_t B_rows, int64_t B_cols, int64_t B_nnz,
+                       const int64_t *B_p, const int64_t *B_i, const double *B_v, int64_t ro_b, int64_t co_b,
+                       double beta, double *C, int64_t ldc, void *stream) {
+    if (layout != 'C' && layout != 'R') return set_error(RBH_ERR_REQUIRE, "(layout is ColMajor or RowMajor) was required, but did not hold, in function right_spmm");
+    if (opB != 'N' && opB != 'T') return set_error(RBH_ERR_REQUIRE, "(opB is NoTrans or Trans) was required, but did not hold, in function right_spmm");
+    return spmm_left<double>(layout == 'C' ? 'R' : 'C', opB == 'N' ? 'T' : 'N', opA, n, m, k, alpha, B_fmt, B_rows,
+                             B_cols, B_nnz, B_p, B_i, B_v, ro_b, co_b, A, lda, beta, C, ldc, stream);
+}
+int rbh_spmm_right_f32(char layout, char opA, char opB, int64_t m, int64_t n, int64_t k, float alpha, const float *A,
+                       int64_t lda, char B_fmt, int64_t B_rows, int64_t B_cols, int64_t B_nnz, const int64_t *B_p,
+                       const int64_t *B_i, const float *B_v, int64_t ro_b, int64_t co_b, float beta, float *C,
+                       int64_t ldc, void *stream) {
+    if (layout != 'C' && layout != 'R') return set_error(RBH_ERR_REQUIRE, "(layout is ColMajor or RowMajor) was required, but did not hold, in function right_spmm");
+    if (opB != 'N' && opB != 'T') return set_error(RBH_ERR_REQUIRE, "(opB is NoTrans or Trans) was required, but did not hold, in function right_spmm");
+    return spmm_left<float>(layout == 'C' ? 'R' : 'C', opB == 'N' ? 'T' : 'N', opA, n, m, k, alpha, B_fmt, B_rows,
+                            B_cols, B_nnz, B_p, B_i, B_v, ro_b, co_b, A, lda, beta, C, ldc, stream);
 }
 
 int rbh_require_symmetric_f64(char layout, const double *A, int64_t n, int64_t lda, double tol, void *stream) {

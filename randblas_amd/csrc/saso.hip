@@ -648,6 +648,22 @@ template <> struct SuAcc<double> {
                      : "m0", "scc");
     }
 };
+// SU_F32_V (diagnostics, with RBH_SASO_F32_UNIT=1 routing f32 here): 0 = xor + index-mode add in
+// one statement; 1 = 0 with s_nop 1 after s_set_gpr_idx_on; 2 = the f64 form (sign flip outside,
+// index-mode add alone); 3 = 0 with s_nop 4 between the xor and s_set_gpr_idx_on.
+#ifndef SU_F32_V
+#define SU_F32_V 0
+#endif
+#if SU_F32_V == 1
+#define SU_F32_NA ""
+#define SU_F32_NB "s_nop 1\n\t"
+#elif SU_F32_V == 3
+#define SU_F32_NA "s_nop 4\n\t"
+#define SU_F32_NB ""
+#else
+#define SU_F32_NA ""
+#define SU_F32_NB ""
+#endif
 template <> struct SuAcc<float> {
     typedef float v32 __attribute__((ext_vector_type(32)));
     v32 a;
@@ -657,16 +673,31 @@ template <> struct SuAcc<float> {
     // the record's SGPR right before s_set_gpr_idx_on lost whole entries).
     __device__ __forceinline__ void add_at(uint32_t rec, float y) {
         if (SU_ABL & 8) { a[0] += __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, y) ^ (rec & 0x80000000u)); return; }
+#if SU_F32_V == 2
+        uint32_t m;
+        asm("s_and_b32 %0, %1, 0x80000000" : "=s"(m) : "s"(rec) : "scc");
+        const float ys = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, y) ^ m);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\t"
+                     "s_set_gpr_idx_on %1, gpr_idx(SRC0,DST)\n\t"
+                     "v_add_f32 v32, v32, %2\n\t"
+                     "s_set_gpr_idx_off"
+                     : "+{v[32:63]}"(a)
+                     : "s"(rec), "v"(ys)
+                     : "m0", "scc");
+#else
         float t;
         asm volatile("v_xor_b32 %1, %3, %4\n\t"
+                     SU_F32_NA
                      "s_waitcnt lgkmcnt(0)\n\t"
                      "s_set_gpr_idx_on %2, gpr_idx(SRC0,DST)\n\t"
+                     SU_F32_NB
                      "v_add_f32 v32, v32, %1\n\t"
                      "s_set_gpr_idx_off"
                      : "+{v[32:63]}"(a), "=&v"(t)
                      : "s"(__builtin_amdgcn_readfirstlane(rec)), "s"(__builtin_amdgcn_readfirstlane(rec & 0x80000000u)),
                        "v"(y)
                      : "m0", "scc");
+#endif
     }
 };
 
@@ -882,11 +913,7 @@ constexpr int SD_RCAP = 2048;
 #define SD_SW_DEF 48   // C3: 0.708 ms with 32-record windows, 0.692 ms with 48 (one window for most waves)
 #endif
 constexpr int SD_SW = SD_SW_DEF;   // records per scalar-load window (32 or 48)
-#if SD_SW_DEF == 48
-#define SD_W32 ""
-#else
-#define SD_W32 "s_waitcnt lgkmcnt(0)"
-#endif (default walk; -DSD_NO_SMEM: LDS records + readlane)
+   // (default walk; -DSD_NO_SMEM: LDS records + readlane)
 // LDS reads of the walk stay in flight across the index-mode add (measured: no effect on the
 // results, 6 % faster than draining them); -DSD_DRAIN_LDS restores the drain
 #ifdef SD_DRAIN_LDS
@@ -1002,9 +1029,12 @@ __device__ __forceinline__ uint32_t lds_addr(const void *ptr) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)ptr;
 }
 // global -> LDS copies: lane l's 16 (4) bytes from g land at LDS byte m0 + 16 l (4 l). M0 is set in
-// the same statement, because the walk's s_set_gpr_idx_on overwrites it.
+// the same statement, because the walk's s_set_gpr_idx_on overwrites it. An SALU write of M0 needs
+// one wait state before an LDS-DMA instruction reads it (the compiler pads this hazard only for its
+// own instructions, never inside an asm string): hence the s_nop 0.
 __device__ __forceinline__ void dma16(const void *g, uint32_t m0) {
     asm volatile("s_mov_b32 m0, %0\n\t"
+                 "s_nop 0\n\t"
                  "global_load_lds_dwordx4 %1, off"
                  :
                  : "s"(m0), "v"(g)
@@ -1012,6 +1042,7 @@ __device__ __forceinline__ void dma16(const void *g, uint32_t m0) {
 }
 __device__ __forceinline__ void dma4(const void *g, uint32_t m0) {
     asm volatile("s_mov_b32 m0, %0\n\t"
+                 "s_nop 0\n\t"
                  "global_load_lds_dword %1, off"
                  :
                  : "s"(m0), "v"(g)
@@ -1210,27 +1241,32 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
             const uint32_t *gw = rec32 + B0 + eb + done;   // rec32 is padded by SD_SW records
             typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
             u32x8 r0, r1, r2, r3;
-            asm volatile("s_load_dwordx8 %0, %4, 0x0\n\t"
-                         "s_load_dwordx8 %1, %4, 0x20\n\t"
-                         "s_load_dwordx8 %2, %4, 0x40\n\t"
-                         "s_load_dwordx8 %3, %4, 0x60\n\t"
-                         SD_W32
-                         : "=&s"(r0), "=&s"(r1), "=&s"(r2), "=&s"(r3)
-                         : "s"(gw)
-                         : "memory");
             uint32_t wr[SD_SW];
             if constexpr (SD_SW == 48) {
-                // the first four loads are still in flight (SD_W32 is empty): the wait here covers
-                // all six, and r0..r3 are tied in so nothing reads them before it
+                // all six loads and their wait in one statement: no SGPR destination is visible to
+                // the compiler before the data has landed
                 u32x8 r4, r5;
-                asm volatile("s_load_dwordx8 %0, %6, 0x80\n\t"
-                             "s_load_dwordx8 %1, %6, 0xa0\n\t"
+                asm volatile("s_load_dwordx8 %0, %6, 0x0\n\t"
+                             "s_load_dwordx8 %1, %6, 0x20\n\t"
+                             "s_load_dwordx8 %2, %6, 0x40\n\t"
+                             "s_load_dwordx8 %3, %6, 0x60\n\t"
+                             "s_load_dwordx8 %4, %6, 0x80\n\t"
+                             "s_load_dwordx8 %5, %6, 0xa0\n\t"
                              "s_waitcnt lgkmcnt(0)"
-                             : "=&s"(r4), "=&s"(r5), "+s"(r0), "+s"(r1), "+s"(r2), "+s"(r3)
+                             : "=&s"(r0), "=&s"(r1), "=&s"(r2), "=&s"(r3), "=&s"(r4), "=&s"(r5)
                              : "s"(gw)
                              : "memory");
 #pragma unroll
                 for (int q = 0; q < 8; ++q) { wr[32 + q] = r4[q]; wr[40 + q] = r5[q]; }
+            } else {
+                asm volatile("s_load_dwordx8 %0, %4, 0x0\n\t"
+                             "s_load_dwordx8 %1, %4, 0x20\n\t"
+                             "s_load_dwordx8 %2, %4, 0x40\n\t"
+                             "s_load_dwordx8 %3, %4, 0x60\n\t"
+                             "s_waitcnt lgkmcnt(0)"
+                             : "=&s"(r0), "=&s"(r1), "=&s"(r2), "=&s"(r3)
+                             : "s"(gw)
+                             : "memory");
             }
 #pragma unroll
             for (int q = 0; q < 8; ++q) { wr[q] = r0[q]; wr[8 + q] = r1[q]; wr[16 + q] = r2[q]; wr[24 + q] = r3[q]; }
@@ -1355,7 +1391,7 @@ static hipError_t run_sparse_dma(const SparseApply &p, const SparseGen *gen, con
     const size_t bytes = (size_t)NV * 16 + (size_t)(NV + 1) * sizeof(int32_t) + (n + SD_SW) * sizeof(uint32_t) + scan_bytes +
                          gen_bytes + 256;
     char *ws = nullptr;
-    err = hipMallocAsync((void **)&ws, bytes, s);
+    err = ws_alloc((void **)&ws, bytes, s);
     if (err != hipSuccess) return err;
     size_t off = 0;
     auto carve = [&](size_t b) { void *q = ws + off; off += (b + 15) & ~(size_t)15; return q; };
@@ -1397,7 +1433,7 @@ static hipError_t run_sparse_dma(const SparseApply &p, const SparseGen *gen, con
         err = hipGetLastError();
         timing_end(s);
     }
-    hipError_t e2 = hipFreeAsync(ws, s);
+    hipError_t e2 = ws_free(ws, s);
     return err != hipSuccess ? err : e2;
 }
 
@@ -1442,7 +1478,7 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
                          n * sizeof(uint16_t) + n * sizeof(uint32_t) + sizeof(UniformTest<T>) +
                          tmp_bytes + 512;
     char *ws = nullptr;
-    err = hipMallocAsync((void **)&ws, bytes, s);
+    err = ws_alloc((void **)&ws, bytes, s);
     if (err != hipSuccess) return err;
     size_t off = 0;
     auto carve = [&](size_t b) { void *q = ws + off; off += (b + 15) & ~(size_t)15; return q; };
@@ -1461,12 +1497,13 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
     const bool y_j = p.ysj == 1;
     const bool y_k = p.ysk == 1 && (p.ysj % VEC) == 0 && (((uintptr_t)p.Y) % 16) == 0 && (p.K % VEC) == 0;
     static const bool unit_off = [] { const char *e = getenv("RBH_NO_SASO_UNIT"); return e && e[0] == '1'; }();
-    // f64 only: the f32 instantiation (index-mode v_add_f32) still loses entries on gfx950 with
-    // nothing in flight, cause not found; f32 takes the general-value kernel
-    const bool unit = (y_j || y_k) && !unit_off && sizeof(T) == 8;
+    // f64 only: the f32 instantiation (index-mode v_add_f32) lost isolated entries on gfx950;
+    // f32 takes the general-value kernel (RBH_SASO_F32_UNIT=1 routes it here for diagnostics)
+    static const bool f32_unit = [] { const char *e = getenv("RBH_SASO_F32_UNIT"); return e && e[0] == '1'; }();
+    const bool unit = (y_j || y_k) && !unit_off && (sizeof(T) == 8 || f32_unit);
 
     err = hipMemsetAsync(ut, 0, sizeof(UniformTest<T>), s);
-    if (err != hipSuccess) { (void)hipFreeAsync(ws, s); return err; }
+    if (err != hipSuccess) { (void)ws_free(ws, s); return err; }
 
     if (nnz > 0) {
         hipLaunchKernelGGL(coo_keys_kernel<T>, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, rows, cols,
@@ -1474,7 +1511,7 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
                            unit ? ut : nullptr);
         // invalid keys (~0) still sort last: their low end_bit bits are all ones, above every valid key
         err = rocprim::radix_sort_pairs(tmp, tmp_bytes, k_in, k_out, v_in, v_out, (size_t)nnz, 0, (unsigned)end_bit, s);
-        if (err != hipSuccess) { (void)hipFreeAsync(ws, s); return err; }
+        if (err != hipSuccess) { (void)ws_free(ws, s); return err; }
     }
     hipLaunchKernelGGL(rowptr_kernel<T>, dim3((unsigned)((nnz + 1 + 255) / 256)), dim3(256), 0, s, nnz, k_out, v_out,
                        NV, p.M, vrp, kl, rec, (uint32_t)sizeof(T));
@@ -1497,7 +1534,7 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
     else hipLaunchKernelGGL((saso_apply_kernel<T, false>), grid, dim3(SA_NT), 0, s, p, vrp, kl, v_out, nchunks, nrb, mixed);
     err = hipGetLastError();
     timing_end(s);
-    hipError_t e2 = hipFreeAsync(ws, s);
+    hipError_t e2 = ws_free(ws, s);
     return err != hipSuccess ? err : e2;
 }
 
@@ -1506,6 +1543,7 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
 // operator is sampled into a workspace and takes the general apply.
 template <typename T>
 static hipError_t run_sparse_sampled_t(const SparseApply &p0, const SparseGen &g, int64_t nnz, hipStream_t s) {
+    if (nnz >= (int64_t)0x7fffffff) return hipErrorInvalidValue;   // int32 CSR offsets (as run_sparse_apply_t)
     SparseApply p = p0;
     p.unit_vals = 1;   // fill_sparse draws values +-1 (sparse_skops.hh:389-413)
     const int64_t long_ax = g.n_rows > g.n_cols ? g.n_rows : g.n_cols;
@@ -1517,7 +1555,7 @@ static hipError_t run_sparse_sampled_t(const SparseApply &p0, const SparseGen &g
         return run_sparse_dma(p, &g, nullptr, nullptr, nullptr, nnz, y_k, s);
     const size_t n = (size_t)(nnz > 0 ? nnz : 1);
     char *ws = nullptr;
-    hipError_t err = hipMallocAsync((void **)&ws, n * (2 * sizeof(int64_t) + sizeof(T)), s);
+    hipError_t err = ws_alloc((void **)&ws, n * (2 * sizeof(int64_t) + sizeof(T)), s);
     if (err != hipSuccess) return err;
     int64_t *gr = (int64_t *)ws;
     int64_t *gc = gr + n;
@@ -1525,7 +1563,7 @@ static hipError_t run_sparse_sampled_t(const SparseApply &p0, const SparseGen &g
     err = launch_fill_sparse_t<T>(g, gr, gc, gv, s);
     // left_spmm returns after the beta scaling when alpha == 0 (spmm_dispatch.hh:134-135)
     if (err == hipSuccess) err = run_sparse_apply_t<T>(p, gr, gc, gv, p.alpha == 0.0 ? 0 : nnz, s);
-    hipError_t e2 = hipFreeAsync(ws, s);
+    hipError_t e2 = ws_free(ws, s);
     return err != hipSuccess ? err : e2;
 }
 

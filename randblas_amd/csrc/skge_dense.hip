@@ -800,7 +800,7 @@ static hipError_t launch_fused(const GemmProblem &p, hipStream_t s) {
     q.partial = nullptr;
     hipError_t e;
     if (split > 1) {
-        e = hipMallocAsync(&q.partial, sizeof(T) * (size_t)split * p.M * p.N, s);
+        e = ws_alloc(&q.partial, sizeof(T) * (size_t)split * p.M * p.N, s);
         if (e != hipSuccess) return e;
     }
     timing_begin(s);
@@ -814,7 +814,7 @@ static hipError_t launch_fused(const GemmProblem &p, hipStream_t s) {
     }
     timing_end(s);
     if (split > 1) {
-        hipError_t e2 = hipFreeAsync(q.partial, s);
+        hipError_t e2 = ws_free(q.partial, s);
         if (e == hipSuccess) e = e2;
     }
     return e;

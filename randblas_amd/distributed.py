@@ -63,3 +63,54 @@ class RowShardedSketch:
             else:
                 src = self.local[c].view(nc, self.d_loc)
             Bv[j0:j1].copy_(src)
+
+
+class ColumnShardedSketch:
+    """Column sharding for the SASO sketch ("SASO partitioning"): rank g owns
+    columns [g*n_loc, (g+1)*n_loc) of A and of B. A sparse operator's columns are pure functions of
+    (seed, k) (sparse_skops.hh:72-92), so every rank samples the same S locally and reads only its
+    own m x n_loc block of A -- no rank reads another's columns. B is ColMajor, so each rank's
+    shard is a contiguous d x n_loc block and the all-gather writes the reassembled sketch with
+    one strided copy per chunk. The all-gather of chunk c overlaps the compute of chunk c+1.
+
+    compute(j0, j1, out) writes the local columns j0 .. j1 (relative to this rank's block) as a
+    ColMajor d x (j1-j0) matrix into the 1-D tensor `out`."""
+
+    def __init__(self, d: int, n_loc: int, compute: Callable[[int, int, torch.Tensor], None],
+                 dtype: torch.dtype, device: torch.device, chunks: int = 4, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.d, self.n_loc = d, n_loc
+        self.compute = compute
+        self.chunks = max(1, min(chunks, n_loc))
+        bounds = [round(i * n_loc / self.chunks) for i in range(self.chunks + 1)]
+        self.cols = [(bounds[i], bounds[i + 1]) for i in range(self.chunks) if bounds[i + 1] > bounds[i]]
+        self.local = [torch.empty(d * (j1 - j0), dtype=dtype, device=device) for j0, j1 in self.cols]
+        self.gathered = [torch.empty(self.world * d * (j1 - j0), dtype=dtype, device=device)
+                         for j0, j1 in self.cols]
+
+    @property
+    def co(self) -> int:
+        """First global column of this rank's block."""
+        return self.rank * self.n_loc
+
+    def __call__(self, B_full: Optional[torch.Tensor]) -> None:
+        """Compute this rank's columns; if B_full (ColMajor d x world*n_loc, 1-D) is given, gather the
+        whole sketch into it on every rank."""
+        works: List = []
+        for c, (j0, j1) in enumerate(self.cols):
+            self.compute(j0, j1, self.local[c])
+            if self.world > 1 and B_full is not None:
+                works.append(dist.all_gather_into_tensor(self.gathered[c], self.local[c], group=self.group,
+                                                         async_op=True))
+        if B_full is None:
+            return
+        Bv = B_full.view(self.world, self.n_loc, self.d)   # [rank][local column][row]
+        for c, (j0, j1) in enumerate(self.cols):
+            nc = j1 - j0
+            if self.world > 1:
+                works[c].wait()
+                Bv[:, j0:j1].copy_(self.gathered[c].view(self.world, nc, self.d))
+            else:
+                Bv[0, j0:j1].copy_(self.local[c].view(nc, self.d))

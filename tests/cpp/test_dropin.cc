@@ -7,6 +7,7 @@
 // Built and run by tests/test_gpu_cpp_dropin.py; prints "ALL PASSED" on success.
 #include <RandBLAS.hh>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <exception>
@@ -254,6 +255,152 @@ static void sparse_data_sketch() {
         }
 }
 
+// Host outputs with padding: only the d x n window of B is written (BLAS semantics). With
+// beta == 0 and ldb > d (ColMajor) / ldb > n (RowMajor), and y with incy > 1, the slots between
+// the window's runs keep the caller's sentinel.
+static void output_padding_untouched() {
+    const int64_t d = 13, m = 70, n = 9;
+    auto A = random_matrix<double>(m, n, 99);
+    for (Layout layout : {Layout::ColMajor, Layout::RowMajor}) {
+        const bool col = layout == Layout::ColMajor;
+        const int64_t lda = col ? m : n, ldb = col ? d + 5 : n + 4;
+        const int64_t ext = col ? ldb * n : ldb * d;
+        std::vector<double> B(ext, std::numeric_limits<double>::quiet_NaN());
+        RandBLAS::DenseSkOp<double> S(RandBLAS::DenseDist(d, m), 3);
+        RandBLAS::sketch_general(layout, Op::NoTrans, Op::NoTrans, d, n, m, 1.0, S, A.data(), lda, 0.0, B.data(), ldb);
+        int64_t in_window_finite = 0, pad_nan = 0, pad = 0;
+        for (int64_t e = 0; e < ext; ++e) {
+            const int64_t inner = e % ldb;
+            const bool in = inner < (col ? d : n);
+            if (in) in_window_finite += std::isfinite(B[e]);
+            else { pad++; pad_nan += std::isnan(B[e]); }
+        }
+        CHECK(in_window_finite == d * n);
+        CHECK(pad_nan == pad);
+        // the same for a sparse operator (sparse apply staging)
+        std::vector<double> Bs(ext, std::numeric_limits<double>::quiet_NaN());
+        RandBLAS::SparseSkOp<double> SS(RandBLAS::SparseDist{d, m, 4}, 5);
+        RandBLAS::sketch_general(layout, Op::NoTrans, Op::NoTrans, d, n, m, 1.0, SS, A.data(), lda, 0.0, Bs.data(), ldb);
+        for (int64_t e = 0; e < ext; ++e) {
+            const bool in = e % ldb < (col ? d : n);
+            CHECK(in ? std::isfinite(Bs[e]) : std::isnan(Bs[e]));
+        }
+    }
+    // sketch_vector: y with incy = 4, beta = 0
+    const int64_t dv = 20, mv = 300, incy = 4;
+    std::vector<double> x(mv, 1.0), y(incy * dv, std::numeric_limits<double>::quiet_NaN());
+    RandBLAS::DenseSkOp<double> Sv(RandBLAS::DenseDist(dv, mv), 8);
+    RandBLAS::sketch_vector(Op::NoTrans, 1.0, Sv, x.data(), (int64_t)1, 0.0, y.data(), incy);
+    for (int64_t e = 0; e < incy * dv; ++e) CHECK((e % incy == 0) ? std::isfinite(y[e]) : std::isnan(y[e]));
+}
+
+// lskges fills an unfilled SparseSkOp (skge.hh:503-504) and the COO apply leaves its arrays sorted
+// in CSC order (coo_spmm_impl.hh:98-103); a transposed application sorts them by (row, col).
+static void sparse_operator_state() {
+    const int64_t d = 17, m = 150, n = 6;
+    RandBLAS::SparseDist D{d, m, 3};
+    auto A = random_matrix<double>(m, n, 99);
+    std::vector<double> B(d * n);
+    RandBLAS::SparseSkOp<double> S(D, 11);
+    CHECK(!S.known_filled);
+    RandBLAS::sketch_general(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, m, 1.0, S, A.data(), m, 0.0, B.data(), d);
+    CHECK(S.known_filled);
+    RandBLAS::SparseSkOp<double> F(D, 11);
+    RandBLAS::fill_sparse(F);
+    const int64_t nnz = F.nnz_count();
+    // expected: F's entries sorted by (col, row)
+    std::vector<int64_t> idx(nnz);
+    for (int64_t e = 0; e < nnz; ++e) idx[e] = e;
+    std::sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) {
+        return F.cols[a] < F.cols[b] || (F.cols[a] == F.cols[b] && F.rows[a] < F.rows[b]);
+    });
+    for (int64_t e = 0; e < nnz; ++e) {
+        CHECK(S.rows[e] == F.rows[idx[e]]);
+        CHECK(S.cols[e] == F.cols[idx[e]]);
+        CHECK(S.vals[e] == F.vals[idx[e]]);
+    }
+    // applying the (now CSC-sorted, known_filled) operator again: same bits, arrays unchanged
+    std::vector<double> B2(d * n);
+    std::vector<int64_t> r0(S.rows, S.rows + nnz);
+    RandBLAS::sketch_general(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, m, 1.0, S, A.data(), m, 0.0, B2.data(), d);
+    for (int64_t e = 0; e < d * n; ++e) CHECK(B2[e] == B[e]);
+    for (int64_t e = 0; e < nnz; ++e) CHECK(S.rows[e] == r0[e]);
+    // opS = Trans on an unfilled operator: the view is transposed, arrays end sorted by (row, col)
+    RandBLAS::SparseSkOp<double> T(RandBLAS::SparseDist{m, d, 3}, 12);
+    std::vector<double> Bt(d * n);
+    RandBLAS::sketch_general(Layout::ColMajor, Op::Trans, Op::NoTrans, d, n, m, 1.0, T, A.data(), m, 0.0, Bt.data(), d);
+    CHECK(T.known_filled);
+    bool rowsorted = true;
+    for (int64_t e = 1; e < T.nnz_count(); ++e)
+        rowsorted = rowsorted && (T.rows[e - 1] < T.rows[e] || (T.rows[e - 1] == T.rows[e] && T.cols[e - 1] < T.cols[e]));
+    CHECK(rowsorted);
+}
+
+// RandBLAS::spmm (spmm_dispatch.hh:290-294, 380-384): sparse on the left and on the right, COO
+// and CSR, against an explicit product with the dense image
+static void spmm_both_sides() {
+    const int64_t m = 40, k = 55, n = 7;
+    std::vector<double> Ad(m * k, 0.0);   // ColMajor image of the sparse A (m x k)
+    std::vector<int64_t> rowptr(m + 1, 0), colidx, crow, ccol;
+    std::vector<double> vals;
+    for (int64_t i = 0; i < m; ++i) {
+        for (int64_t j = 0; j < k; ++j)
+            if ((i * 5 + j * 7) % 13 == 0) {
+                const double v = 0.5 * (double)((i + 3 * j) % 7) - 1.5;
+                colidx.push_back(j); crow.push_back(i); ccol.push_back(j); vals.push_back(v);
+                Ad[i + j * m] = v;
+            }
+        rowptr[i + 1] = (int64_t)colidx.size();
+    }
+    const int64_t nnz = (int64_t)vals.size();
+    RandBLAS::CSRMatrix<double> Acsr(m, k, nnz, vals.data(), rowptr.data(), colidx.data());
+    std::vector<double> cv(vals);
+    RandBLAS::COOMatrix<double> Acoo(m, k, nnz, cv.data(), crow.data(), ccol.data());
+    auto Bd = random_matrix<double>(k, n, 3);
+    const double eps = std::numeric_limits<double>::epsilon();
+    // left: C (m x n) = 2 A B - C0
+    auto C0 = random_matrix<double>(m, n, 4);
+    for (int pass = 0; pass < 2; ++pass) {
+        std::vector<double> C(C0);
+        if (pass == 0)
+            RandBLAS::spmm(Layout::ColMajor, Op::NoTrans, Op::NoTrans, m, n, k, 2.0, Acsr, 0, 0, Bd.data(), k, -1.0, C.data(), m);
+        else
+            RandBLAS::spmm(Layout::ColMajor, Op::NoTrans, Op::NoTrans, m, n, k, 2.0, Acoo, 0, 0, Bd.data(), k, -1.0, C.data(), m);
+        for (int64_t i = 0; i < m; ++i)
+            for (int64_t j = 0; j < n; ++j) {
+                double ex = -C0[i + j * m], bound = std::fabs(C0[i + j * m]) * eps;
+                for (int64_t c = 0; c < k; ++c) {
+                    ex += 2.0 * Ad[i + c * m] * Bd[c + j * k];
+                    bound += std::fabs(2.0 * Ad[i + c * m] * Bd[c + j * k]) * k * 2 * eps;
+                }
+                CHECK(std::fabs(C[i + j * m] - ex) <= bound + 1e-300);
+            }
+    }
+    // right: C (n2 x k) = D (n2 x m) A (m x k), ColMajor
+    const int64_t n2 = 6;
+    auto Dd = random_matrix<double>(n2, m, 5);
+    std::vector<double> C(n2 * k, 0.0);
+    RandBLAS::spmm(Layout::ColMajor, Op::NoTrans, Op::NoTrans, n2, k, m, 1.0, Dd.data(), n2, Acsr, 0, 0, 0.0, C.data(), n2);
+    for (int64_t i = 0; i < n2; ++i)
+        for (int64_t j = 0; j < k; ++j) {
+            double ex = 0, bound = 0;
+            for (int64_t c = 0; c < m; ++c) {
+                ex += Dd[i + c * n2] * Ad[c + j * m];
+                bound += std::fabs(Dd[i + c * n2] * Ad[c + j * m]);
+            }
+            CHECK(std::fabs(C[i + j * n2] - ex) <= bound * m * 2 * eps + 1e-300);
+        }
+    // left_spmm's CSR requirement: exact dimensions and zero offsets (spmm_dispatch.hh:100-103)
+    bool threw = false;
+    try {
+        std::vector<double> Cx(m * n);
+        RandBLAS::spmm(Layout::ColMajor, Op::NoTrans, Op::NoTrans, m - 1, n, k, 1.0, Acsr, 1, 0, Bd.data(), k, 0.0, Cx.data(), m);
+    } catch (RandBLAS::exceptions::Error &e) {
+        threw = std::string(e.what()).find("was required, but did not hold") != std::string::npos;
+    }
+    CHECK(threw);
+}
+
 int main() {
 #ifdef ONLY_SKSP   // diagnostics: the sketch_sparse checks alone
     try {
@@ -273,6 +420,9 @@ int main() {
     symmetric_and_errors();
     vector_sketch();
     sparse_data_sketch();
+    output_padding_untouched();
+    sparse_operator_state();
+    spmm_both_sides();
     if (g_fail) {
         std::printf("%d checks FAILED\n", g_fail);
         return 1;

@@ -1,0 +1,30 @@
+"""bench.py's multi-rank launch path on the CPU: `--gpus 2` outside torchrun relaunches itself as two
+ranks under torch.distributed.run (127.0.0.1 rendezvous), both ranks join (gloo in --dry-run, which
+does no device work), the max-over-ranks reduction runs and rank 0 reports n_gpus = 2. A world size
+that disagrees with --gpus is refused."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env=None):
+    e = dict(os.environ)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=240, env=e)
+
+
+def test_bench_relaunches_n_ranks():
+    r = _run(["--gpus", "2", "--dry-run", "--config", "c3", "--steps", "1", "--warmup", "0"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    assert lines[0]["n_gpus"] == 2 and lines[0]["ranks_max"] == 1.0 and lines[0]["dry_run"] is True
+
+
+def test_bench_refuses_world_mismatch():
+    r = _run(["--gpus", "4", "--dry-run"], env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2

@@ -86,3 +86,59 @@ def test_row_sharded_gloo_world2(kind, chunks):
             assert np.array_equal(results[r], exp)
         else:
             np.testing.assert_allclose(results[r], exp, rtol=1e-13, atol=1e-13)
+
+
+def _col_worker(rank, world, port, chunks, q):
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    sys.path.insert(0, os.path.dirname(here))
+    import oracle_lib as O
+    from randblas_amd.distributed import ColumnShardedSketch
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    d, m, n_loc = 40, 260, 23
+    n = world * n_loc
+    A = O.random_matrix(m, n, 99)
+    rows, cols, vals = O.fill_sparse(d, m, 5, "S", key=0)
+
+    def compute(j0, j1, out):   # this rank's block only: global columns co + j0 .. co + j1
+        g0 = rank * n_loc + j0
+        Ach = np.ascontiguousarray(A[g0 * m:(g0 + j1 - j0) * m])
+        O.left_spmm_coo("C", "N", "N", d, j1 - j0, m, 1.0, d, m, rows, cols, vals, 0, 0, Ach, m, 0.0, out.numpy(), d)
+
+    drv = ColumnShardedSketch(d, n_loc, compute, torch.float64, torch.device("cpu"), chunks=chunks)
+    B = torch.zeros(d * n, dtype=torch.float64)
+    drv(B)
+    q.put((rank, B.numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("chunks", [1, 4])
+def test_column_sharded_saso_gloo_world2(chunks):
+    """SASO column shard: each rank reads only its columns of A; the gathered
+    sketch is bitwise the unsharded one on every rank."""
+    import oracle_lib as O
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_col_worker, args=(r, world, port, chunks, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    d, m, n = 40, 260, 2 * 23
+    A = O.random_matrix(m, n, 99)
+    rows, cols, vals = O.fill_sparse(d, m, 5, "S", key=0)
+    exp = np.zeros(d * n)
+    O.left_spmm_coo("C", "N", "N", d, n, m, 1.0, d, m, rows, cols, vals, 0, 0, A, m, 0.0, exp, d)
+    for r in range(world):
+        assert np.array_equal(results[r], exp)

@@ -85,7 +85,11 @@ def run_case(cuda, side, layout, fmt, opS, opA, dtype, alpha, beta, dims, offs, 
     ssR, ssC = (sR, sC) if opS == "N" else (sC, sR)
     saR, saC = (aR, aC) if opA == "N" else (aC, aR)
     SR, SC = ssR + ro_s + 2, ssC + co_s + 1
-    AR, AC = saR + ro_a + 1, saC + co_a + 3
+    if fmt == "COO":
+        AR, AC = saR + ro_a + 1, saC + co_a + 3
+    else:   # left_spmm's CSR / CSC branch takes the whole matrix only (spmm_dispatch.hh:100-103)
+        ro_a = co_a = 0
+        AR, AC = saR, saC
     rows, cols, vals, Adense = random_sparse(AR, AC, 0.08, 7, dtype)
     A = as_format(fmt, AR, AC, rows, cols, vals, cuda)
     if identity:
@@ -173,3 +177,10 @@ def test_sketch_sparse_alpha_zero_and_errors(cuda):
         rb.sketch_sparse("C", "N", "N", 10, 40, 50, 1.0, S, A, 0.0, dB, 10, ro_a=1)
     with pytest.raises(rb.RandBLASError):   # ldb < d
         rb.sketch_sparse("C", "N", "N", 10, 40, 50, 1.0, S, A, 0.0, dB, 9)
+    # CSR / CSC data: a window (or offsets) is refused, as left_spmm requires (spmm_dispatch.hh:100-103)
+    for fmt in ("CSR", "CSC"):
+        Af = as_format(fmt, 50, 40, rows, cols, vals, cuda)
+        with pytest.raises(rb.RandBLASError, match="left_spmm"):
+            rb.sketch_sparse("C", "N", "N", 10, 39, 50, 1.0, S, Af, 0.0, dB, 10)
+        with pytest.raises(rb.RandBLASError, match="left_spmm"):
+            rb.sketch_sparse("C", "N", "N", 10, 39, 50, 1.0, S, Af, 0.0, dB, 10, co_a=1)
