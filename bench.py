@@ -51,6 +51,7 @@ CONFIGS = {
     "c3": ("saso", "f64", 1024, 16384, 16384, 8),
     "c4": ("dense", "f32", 256, 32768, 32768, 0),    # per GPU: d = 2048 at N = 8 (configs[3])
     "c5": ("sksy", "f64", 512, 16384, 16384, 0),
+    "c5p": ("sksyp", "f64", 512, 16384, 16384, 0),   # configs[4] as worded: packed-symmetric A
 }
 
 
@@ -195,10 +196,15 @@ def main():
     else:
         rb.fill_dense("C", rb.DenseDist(m, n), m, n, 0, 0, A, rb.RNGState(99))
         S = rb.DenseSkOp(rb.DenseDist(world * d, m), rb.RNGState(0))
-    if kind == "sksy":   # A symmetric: A := (A + A^T) / 2 (input prep, not timed)
+    if kind in ("sksy", "sksyp"):   # A symmetric: A := (A + A^T) / 2 (input prep, not timed)
         Am = A.view(n, m)
         A.copy_(((Am + Am.t()) * 0.5).reshape(-1))
         del Am
+    if kind == "sksyp":   # BLAS packed upper triangle, ColMajor: column j's A(0..j, j) in turn
+        Av = A.view(n, m)   # row j of the view = column j of A
+        A = Av.masked_select(torch.ones(n, n, dtype=torch.bool, device=dev).tril()).contiguous()
+        del Av
+        torch.cuda.empty_cache()
 
     k_ev = []   # (start, end) HIP events around every library call of the timed steps
 
@@ -220,10 +226,16 @@ def main():
         timed(lambda: rb.sketch_general_left("C", "N", "N", d, j1 - j0, m, 1.0, S, Ach, m, 0.0, out, d, ro_s=ro_s),
               record)
 
-    def symcheck(record=False):
-        # sketch_symmetric's util::require_symmetric with the reference's default tol = 0
-        # (sksy.hh:520-537, util.hh:165-188): part of every C5 step, timed with it
-        timed(lambda: rb.require_symmetric("C", A, n, n, 0.0), record)
+    def sksy(ro_s, out, record=False):
+        """One sketch_symmetric call (sksy.hh:520-537) with the reference's default sym_check_tol = 0:
+        the device symmetry check, then the sketch, which reads only A's upper triangle once the
+        check has found A bitwise symmetric."""
+        timed(lambda: rb.sketch_symmetric_left("C", d, n, 1.0, S, A, n, 0.0, out, d, ro_s=ro_s, sym_check_tol=0.0),
+              record)
+
+    def sksyp(ro_s, out, record=False):
+        """The packed-symmetric sketch (rbh_sksy_tri, the one-triangle kernel on packed storage)."""
+        timed(lambda: rb.sketch_symmetric_tri("C", "L", "U", "P", d, n, 1.0, S, A, 0, 0.0, out, d, ro_s=ro_s), record)
 
     recording = [False]
     if world > 1 and kind == "saso":
@@ -240,21 +252,27 @@ def main():
         from randblas_amd.distributed import RowShardedSketch
 
         B_full = torch.empty(world * d * n, dtype=tdt, device=dev)
-        drv = RowShardedSketch(world * d, n, lambda ro, j0, j1, out: compute(ro, j0, j1, out, recording[0]),
-                               tdt, dev, chunks=args.chunks)
+        if kind in ("sksy", "sksyp"):   # the symmetric sketch takes the whole square A: one chunk per rank
+            fn = sksy if kind == "sksy" else sksyp
+            drv = RowShardedSketch(world * d, n, lambda ro, j0, j1, out: fn(ro, out, recording[0]), tdt, dev,
+                                   chunks=1)
+        else:
+            drv = RowShardedSketch(world * d, n, lambda ro, j0, j1, out: compute(ro, j0, j1, out, recording[0]),
+                                   tdt, dev, chunks=args.chunks)
 
         def step(record=False):
             recording[0] = record
-            if kind == "sksy":
-                symcheck(record)
             drv(B_full)
     else:
         B = torch.empty(d * n, dtype=tdt, device=dev)
 
         def step(record=False):
             if kind == "sksy":
-                symcheck(record)
-            compute(0, 0, n, B, record)
+                sksy(0, B, record)
+            elif kind == "sksyp":
+                sksyp(0, B, record)
+            else:
+                compute(0, 0, n, B, record)
 
     for _ in range(args.warmup):
         step()
@@ -328,11 +346,13 @@ def main():
                                     "ns": "Gaussian skge fp64 north-star",
                                     "c3": "SASO SparseSkOp vec_nnz=8 fp64 (configs[2])",
                                     "c4": "Gaussian skge fp32 (configs[3])",
-                                    "c5": "sksy fp64 (configs[4])"}[args.config],
+                                    "c5": "sksy fp64, sketch_symmetric with sym_check_tol=0 (configs[4])",
+                                    "c5p": "sksy fp64 on packed-symmetric A (configs[4] as worded)"}[args.config],
                        "d": d if kind == "saso" else world * d, "d_per_gpu": d, "m": m,
                        "n": world * n if kind == "saso" else n, "n_per_gpu": n, "layout": "ColMajor",
                        "operator": "SparseSkOp SASO" if kind == "saso" else "DenseSkOp Gaussian MajorAxis::Long",
-                       "symmetry_check": "tol=0 (timed in the step)" if kind == "sksy" else None,
+                       "symmetry_check": ("tol=0, timed in the step" if kind == "sksy" else None),
+                       "A_storage": {"sksy": "full", "sksyp": "packed upper (n(n+1)/2)"}.get(kind, "full"),
                        "parallelism": (f"{'column' if kind == 'saso' else 'row'}-shard x{world} + RCCL all-gather"
                                        if world > 1 else "single GPU")},
             "pct_of_peak": roof["frac"] * 100.0,

@@ -37,6 +37,8 @@
 namespace blas {
 enum class Layout : char { ColMajor = 'C', RowMajor = 'R' };
 enum class Op : char { NoTrans = 'N', Trans = 'T', ConjTrans = 'C' };
+enum class Uplo : char { Upper = 'U', Lower = 'L', General = 'G' };
+enum class Side : char { Left = 'L', Right = 'R' };
 }  // namespace blas
 
 // ---------------------------------------------------------------------------------------------
@@ -239,6 +241,8 @@ template <> struct Api<double> {
     static constexpr auto sym = rbh_require_symmetric_f64;
     static constexpr auto lsksp3 = rbh_lsksp3_f64;
     static constexpr auto rsksp3 = rbh_rsksp3_f64;
+    static constexpr auto sksy = rbh_sketch_symmetric_f64;
+    static constexpr auto sksy_tri = rbh_sksy_tri_f64;
 };
 template <> struct Api<float> {
     static int fill_dense(char l, const rbh_dense_dist *D, int64_t r, int64_t c, int64_t ro, int64_t co, float *b,
@@ -253,6 +257,8 @@ template <> struct Api<float> {
     static constexpr auto sym = rbh_require_symmetric_f32;
     static constexpr auto lsksp3 = rbh_lsksp3_f32;
     static constexpr auto rsksp3 = rbh_rsksp3_f32;
+    static constexpr auto sksy = rbh_sketch_symmetric_f32;
+    static constexpr auto sksy_tri = rbh_sksy_tri_f32;
 };
 }  // namespace detail
 
@@ -523,41 +529,71 @@ void require_symmetric(blas::Layout layout, const T *A, int64_t n, int64_t lda, 
 }
 }  // namespace util
 
+namespace detail {
+// the check + sketch of sksy.hh in one C-ABI call for a dense operator (which reads one triangle
+// of A once the check has found it bitwise symmetric); a sparse operator: check + sketch_general
+template <typename T, typename RNG>
+void sksy(blas::Layout layout, char side, int64_t d, int64_t n, T alpha, DenseSkOp<T, RNG> &S, int64_t ro_s,
+          int64_t co_s, const T *A, int64_t lda, T beta, T *B, int64_t ldb, T tol) {
+    const rbh_dense_dist dd = c_dist(S.dist);
+    const rbh_state s = c_state(S.seed_state);
+    check(Api<T>::sksy((char)layout, side, d, n, alpha, &dd, &s, S.buff, (char)S.layout, ro_s, co_s, A, lda, beta, B,
+                       ldb, tol, nullptr));
+}
+template <typename T, typename RNG, typename sint_t>
+void sksy(blas::Layout layout, char side, int64_t d, int64_t n, T alpha, SparseSkOp<T, RNG, sint_t> &S, int64_t ro_s,
+          int64_t co_s, const T *A, int64_t lda, T beta, T *B, int64_t ldb, T tol) {
+    util::require_symmetric(layout, A, n, lda, tol);
+    if (side == 'L') lsk(layout, blas::Op::NoTrans, blas::Op::NoTrans, d, n, n, alpha, S, ro_s, co_s, A, lda, beta, B, ldb);
+    else rsk(layout, blas::Op::NoTrans, blas::Op::NoTrans, n, d, n, alpha, A, lda, S, ro_s, co_s, beta, B, ldb);
+}
+}  // namespace detail
+
 // B = alpha A op(submat(S)) + beta B   (A symmetric n x n in general storage)
 template <typename T, typename SKOP>
 inline void sketch_symmetric(blas::Layout layout, int64_t n, int64_t d, T alpha, const T *A, int64_t lda, SKOP &S,
                              int64_t ro_s, int64_t co_s, T beta, T *B, int64_t ldb, T sym_check_tol = 0) {
-    util::require_symmetric(layout, A, n, lda, sym_check_tol);
-    sketch_general(layout, blas::Op::NoTrans, blas::Op::NoTrans, n, d, n, alpha, A, lda, S, ro_s, co_s, beta, B, ldb);
+    detail::sksy(layout, 'R', d, n, alpha, S, ro_s, co_s, A, lda, beta, B, ldb, sym_check_tol);
 }
 
 // B = alpha submat(S) A + beta B
 template <typename T, typename SKOP>
 inline void sketch_symmetric(blas::Layout layout, int64_t d, int64_t n, T alpha, SKOP &S, int64_t ro_s, int64_t co_s,
                              const T *A, int64_t lda, T beta, T *B, int64_t ldb, T sym_check_tol = 0) {
-    util::require_symmetric(layout, A, n, lda, sym_check_tol);
-    sketch_general(layout, blas::Op::NoTrans, blas::Op::NoTrans, d, n, n, alpha, S, ro_s, co_s, A, lda, beta, B, ldb);
+    detail::sksy(layout, 'L', d, n, alpha, S, ro_s, co_s, A, lda, beta, B, ldb, sym_check_tol);
 }
 
 // B = alpha A S + beta B
 template <typename T, typename SKOP>
 inline void sketch_symmetric(blas::Layout layout, T alpha, const T *A, int64_t lda, SKOP &S, T beta, T *B,
                              int64_t ldb, T sym_check_tol = 0) {
-    const int64_t n = S.dist.n_rows, d = S.dist.n_cols;
-    util::require_symmetric(layout, A, n, lda, sym_check_tol);
-    sketch_general(layout, blas::Op::NoTrans, blas::Op::NoTrans, n, d, n, alpha, A, lda, S, (int64_t)0, (int64_t)0,
-                   beta, B, ldb);
+    detail::sksy(layout, 'R', S.dist.n_cols, S.dist.n_rows, alpha, S, (int64_t)0, (int64_t)0, A, lda, beta, B, ldb,
+                 sym_check_tol);
 }
 
 // B = alpha S A + beta B
 template <typename T, typename SKOP>
 inline void sketch_symmetric(blas::Layout layout, T alpha, SKOP &S, const T *A, int64_t lda, T beta, T *B,
                              int64_t ldb, T sym_check_tol = 0) {
-    const int64_t d = S.dist.n_rows, n = S.dist.n_cols;
-    util::require_symmetric(layout, A, n, lda, sym_check_tol);
-    sketch_general(layout, blas::Op::NoTrans, blas::Op::NoTrans, d, n, n, alpha, S, (int64_t)0, (int64_t)0, A, lda,
-                   beta, B, ldb);
+    detail::sksy(layout, 'L', S.dist.n_rows, S.dist.n_cols, alpha, S, (int64_t)0, (int64_t)0, A, lda, beta, B, ldb,
+                 sym_check_tol);
 }
+
+// Extension (no reference counterpart): a symmetric sketch that reads only triangle `uplo` of A,
+// in full storage (lda) or, with `packed`, in BLAS packed storage (n (n + 1) / 2 entries, lda
+// ignored). side Left: B (d x n) = alpha submat(S) A + beta B; Right: B (n x d) = alpha A submat(S)
+// + beta B. No symmetry check (the other triangle is never read).
+namespace ext {
+template <typename T, typename RNG>
+inline void sketch_symmetric_triangle(blas::Side side, blas::Layout layout, blas::Uplo uplo, bool packed, int64_t d,
+                                      int64_t n, T alpha, DenseSkOp<T, RNG> &S, int64_t ro_s, int64_t co_s, const T *A,
+                                      int64_t lda, T beta, T *B, int64_t ldb) {
+    const rbh_dense_dist dd = c_dist(S.dist);
+    const rbh_state s = detail::c_state(S.seed_state);
+    detail::check(detail::Api<T>::sksy_tri((char)layout, (char)side, (char)uplo, packed ? 'P' : 'F', d, n, alpha, &dd,
+                                           &s, S.buff, (char)S.layout, ro_s, co_s, A, lda, beta, B, ldb, nullptr));
+}
+}  // namespace ext
 
 // ---------------------------------------------------------------------------------------------
 // sketch_vector (skve.hh:152-258): sketch_general in RowMajor with n = 1, lda = incx, ldb = incy

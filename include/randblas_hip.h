@@ -207,6 +207,30 @@ int rbh_spmm_right_f32(char layout, char opA, char opB, int64_t m, int64_t n, in
 /* util::require_symmetric (util.hh:165-188) on the device: RBH_OK if |A_ij - A_ji| <=
  * (|A_ij| + |A_ji| + 1) * tol for all i < j (tol < 0 skips the check), else RBH_ERR_SYMMETRY.
  * sketch_symmetric (sksy.hh:165-537) = this check + the sketch_general entry points above. */
+/* sketch_symmetric in one call (sksy.hh:165-537): require_symmetric with sym_check_tol (skipped when
+ * negative), then side 'L': B (d x n) = alpha * submat(S) * A + beta * B (sksy.hh:300-319, 520-537) or
+ * side 'R': B (n x d) = alpha * A * submat(S) + beta * B (sksy.hh:165-184, 413-430), submat(S) at
+ * (ro_s, co_s) of S ~ D, A n x n full storage in `layout`. RBH_ERR_SYMMETRY when the check fails.
+ * (The check also notes whether A is bitwise symmetric; with RBH_SKSY_TRI=1 in the environment
+ * only the upper triangle of such an A is read, which gives the same bits.) */
+int rbh_sketch_symmetric_f64(char layout, char side, int64_t d, int64_t n, double alpha, const rbh_dense_dist *D,
+                             const rbh_state *seed, const double *S_buff, char S_layout, int64_t ro_s, int64_t co_s,
+                             const double *A, int64_t lda, double beta, double *B, int64_t ldb, double sym_check_tol,
+                             void *stream);
+int rbh_sketch_symmetric_f32(char layout, char side, int64_t d, int64_t n, float alpha, const rbh_dense_dist *D,
+                             const rbh_state *seed, const float *S_buff, char S_layout, int64_t ro_s, int64_t co_s,
+                             const float *A, int64_t lda, float beta, float *B, int64_t ldb, float sym_check_tol,
+                             void *stream);
+/* Extension (no reference counterpart; BASELINE configs[4]'s packed-symmetric A): the same sketch
+ * with only triangle `uplo` ('U'/'L', of A in `layout`) of A read and no symmetry check: A_fmt 'F'
+ * full storage with lda (the other triangle is never touched and may hold anything), 'P' BLAS
+ * packed storage of that triangle (n (n + 1) / 2 entries; lda ignored). */
+int rbh_sksy_tri_f64(char layout, char side, char uplo, char A_fmt, int64_t d, int64_t n, double alpha,
+                     const rbh_dense_dist *D, const rbh_state *seed, const double *S_buff, char S_layout, int64_t ro_s,
+                     int64_t co_s, const double *A, int64_t lda, double beta, double *B, int64_t ldb, void *stream);
+int rbh_sksy_tri_f32(char layout, char side, char uplo, char A_fmt, int64_t d, int64_t n, float alpha,
+                     const rbh_dense_dist *D, const rbh_state *seed, const float *S_buff, char S_layout, int64_t ro_s,
+                     int64_t co_s, const float *A, int64_t lda, float beta, float *B, int64_t ldb, void *stream);
 int rbh_require_symmetric_f64(char layout, const double *A, int64_t n, int64_t lda, double tol, void *stream);
 int rbh_require_symmetric_f32(char layout, const float *A, int64_t n, int64_t lda, float tol, void *stream);
 

@@ -108,6 +108,13 @@ for _t, _ct in (("f64", ctypes.c_double), ("f32", ctypes.c_float)):
     getattr(lib, f"rbh_spmm_right_{_t}").argtypes = [c_char, c_char, c_char, c_i64, c_i64, c_i64, _ct, c_vp, c_i64] + \
         _spm + [_ct, c_vp, c_i64, c_vp]
 lib.rbh_is_device_pointer.argtypes = [c_vp]
+for _t, _ct in (("f64", ctypes.c_double), ("f32", ctypes.c_float)):
+    getattr(lib, f"rbh_sketch_symmetric_{_t}").argtypes = [c_char, c_char, c_i64, c_i64, _ct, P(DenseDistC),
+                                                           P(RNGStateC), c_vp, c_char, c_i64, c_i64, c_vp, c_i64, _ct,
+                                                           c_vp, c_i64, _ct, c_vp]
+    getattr(lib, f"rbh_sksy_tri_{_t}").argtypes = [c_char, c_char, c_char, c_char, c_i64, c_i64, _ct, P(DenseDistC),
+                                                   P(RNGStateC), c_vp, c_char, c_i64, c_i64, c_vp, c_i64, _ct, c_vp,
+                                                   c_i64, c_vp]
 
 # --------------------------------------------------------------------------------------------
 # Python mirror of the reference's types
@@ -337,18 +344,41 @@ def require_symmetric(layout, A, n, lda, tol, stream=None) -> None:
     _check(fn(_b(layout), _ptr(A), n, lda, tol, _stream(A, stream)))
 
 
+def _sksy(side, layout, d, n, alpha, S, A, lda, beta, B, ldb, ro_s, co_s, tol, stream):
+    if not isinstance(S, DenseSkOp):
+        # a SparseSkOp: require_symmetric + the sparse sketch_general (sksy.hh's SKOP is any operator)
+        require_symmetric(layout, A, n, lda, tol, stream)
+        if side == "L":
+            return sketch_general_left(layout, "N", "N", d, n, n, alpha, S, A, lda, beta, B, ldb, ro_s, co_s, stream)
+        return sketch_general_right(layout, "N", "N", n, d, n, alpha, A, lda, S, beta, B, ldb, ro_s, co_s, stream)
+    t = _dtype_tag(B)
+    _check(getattr(lib, f"rbh_sketch_symmetric_{t}")(_b(layout), _b(side), d, n, alpha, ctypes.byref(S.dist.c()),
+                                                     ctypes.byref(S.seed_state.c()), _ptr(S.buff), _b(S.buff_layout),
+                                                     ro_s, co_s, _ptr(A), lda, beta, _ptr(B), ldb, tol,
+                                                     _stream(B, stream)))
+
+
 def sketch_symmetric_left(layout, d, n, alpha, S, A, lda, beta, B, ldb, ro_s=0, co_s=0, sym_check_tol=0.0,
                           stream=None):
     """B = alpha S A + beta B, A symmetric n x n in general storage (sksy.hh:300-319 / 520-537)."""
-    require_symmetric(layout, A, n, lda, sym_check_tol, stream)
-    sketch_general_left(layout, "N", "N", d, n, n, alpha, S, A, lda, beta, B, ldb, ro_s, co_s, stream)
+    _sksy("L", layout, d, n, alpha, S, A, lda, beta, B, ldb, ro_s, co_s, sym_check_tol, stream)
 
 
 def sketch_symmetric_right(layout, n, d, alpha, A, lda, S, beta, B, ldb, ro_s=0, co_s=0, sym_check_tol=0.0,
                            stream=None):
     """B = alpha A S + beta B, A symmetric n x n in general storage (sksy.hh:165-184 / 413-430)."""
-    require_symmetric(layout, A, n, lda, sym_check_tol, stream)
-    sketch_general_right(layout, "N", "N", n, d, n, alpha, A, lda, S, beta, B, ldb, ro_s, co_s, stream)
+    _sksy("R", layout, d, n, alpha, S, A, lda, beta, B, ldb, ro_s, co_s, sym_check_tol, stream)
+
+
+def sketch_symmetric_tri(layout, side, uplo, A_fmt, d, n, alpha, S, A, lda, beta, B, ldb, ro_s=0, co_s=0,
+                         stream=None):
+    """Extension: the symmetric sketch reading only triangle `uplo` of A ('F' full storage, 'P' packed);
+    side 'L': B = alpha submat(S) A + beta B (d x n), 'R': B = alpha A submat(S) + beta B (n x d)."""
+    t = _dtype_tag(B)
+    _check(getattr(lib, f"rbh_sksy_tri_{t}")(_b(layout), _b(side), _b(uplo), _b(A_fmt), d, n, alpha,
+                                             ctypes.byref(S.dist.c()), ctypes.byref(S.seed_state.c()), _ptr(S.buff),
+                                             _b(S.buff_layout), ro_s, co_s, _ptr(A), lda, beta, _ptr(B), ldb,
+                                             _stream(B, stream)))
 
 
 def sketch_general(layout, op1, op2, d_or_m, n_or_d, m_or_n, alpha, X, Y, lda_or_none, *args, **kw):
@@ -502,4 +532,5 @@ __all__ = [
     "sketch_symmetric_right", "require_symmetric", "dense_next_state", "sparse_next_state", "abi_version", "lib",
     "LIB_PATH", "kernel_timing", "kernel_times_ms", "sketch_vector", "sketch_vector_full", "COOMatrix",
     "CSRMatrix", "CSCMatrix", "sketch_sparse", "sketch_sparse_left", "sketch_sparse_right", "spmm",
+    "sketch_symmetric_tri",
 ]

@@ -56,8 +56,11 @@ void timing_end(hipStream_t s) {
 }
 
 // Workspaces: one stream-ordered pool per device, created on first use and private to this
-// library. It keeps up to RBH_POOL_KEEP_BYTES (default 1 GiB) of freed memory across
-// synchronisations, so repeated calls reuse their workspaces instead of remapping them.
+// library (the client's default pool is never touched). The pool never returns memory to the
+// system (release threshold = max): with a threshold of 0 it trims at every synchronisation, and a
+// block allocated after such a trim was observed to lose a kernel's writes in a C++ client that
+// also stages host arrays through hipMalloc (B read back as zeros; memset of the fresh block then
+// faulted). DESIGN.md §7 records the study; RBH_POOL_KEEP_BYTES overrides the threshold for it.
 namespace {
 std::mutex g_pool_mu;
 hipMemPool_t g_pool[64] = {};
@@ -79,14 +82,32 @@ hipError_t ws_alloc(void **p, size_t bytes, hipStream_t s) {
             e = hipMemPoolCreate(&g_pool[dev], &props);
             if (e != hipSuccess) { g_pool[dev] = nullptr; return e; }
             const char *k = getenv("RBH_POOL_KEEP_BYTES");
-            uint64_t keep = k ? strtoull(k, nullptr, 10) : (1ull << 30);
+            uint64_t keep = k ? strtoull(k, nullptr, 10) : UINT64_MAX;
             (void)hipMemPoolSetAttribute(g_pool[dev], hipMemPoolAttrReleaseThreshold, &keep);
         }
         pool = g_pool[dev];
     }
-    return hipMallocFromPoolAsync(p, bytes, pool, s);
+    // diagnostics (the pool-trim study): RBH_WS_MODE=legacy takes workspaces from
+    // hipMalloc; =sync synchronises the stream after each pool allocation; =zero memsets it
+    static const int mode = [] {
+        const char *m = getenv("RBH_WS_MODE");
+        return !m ? 0 : (!strcmp(m, "legacy") ? 1 : (!strcmp(m, "sync") ? 2 : (!strcmp(m, "zero") ? 3 : 0)));
+    }();
+    if (mode == 1) return hipMalloc(p, bytes);
+    e = hipMallocFromPoolAsync(p, bytes, pool, s);
+    if (e == hipSuccess && mode == 2) e = hipStreamSynchronize(s);
+    if (e == hipSuccess && mode == 3) e = hipMemsetAsync(*p, 0, bytes, s);
+    return e;
 }
-hipError_t ws_free(void *p, hipStream_t s) { return p ? hipFreeAsync(p, s) : hipSuccess; }
+hipError_t ws_free(void *p, hipStream_t s) {
+    static const bool legacy = [] { const char *m = getenv("RBH_WS_MODE"); return m && !strcmp(m, "legacy"); }();
+    if (!p) return hipSuccess;
+    if (legacy) {
+        hipError_t e = hipStreamSynchronize(s);
+        return e == hipSuccess ? hipFree(p) : e;
+    }
+    return hipFreeAsync(p, s);
+}
 }  // namespace rbh
 
 namespace {
@@ -289,6 +310,15 @@ int run_dense(GemmProblem &p, hipStream_t s) {
     return RBH_OK;
 }
 
+template <typename T>
+void build_left(GemmProblem &p, char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, T alpha, T beta,
+                const rbh_dense_dist *D, const rbh_state *seed, const void *dS, char S_layout, int64_t ro_s,
+                int64_t co_s, const void *dA, int64_t lda, void *dB, int64_t ldb);
+template <typename T>
+void build_right(GemmProblem &p, char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, T alpha, T beta,
+                 const void *dA, int64_t lda, const rbh_dense_dist *D, const rbh_state *seed, const void *dS,
+                 char S_layout, int64_t ro_s, int64_t co_s, void *dB, int64_t ldb);
+
 // ---------------------------------------------------------------------------------------------
 // dense left: B = alpha op(submat(S)) op(A) + beta B        (dense::lskge3, skge.hh:173-215)
 // ---------------------------------------------------------------------------------------------
@@ -325,8 +355,20 @@ int lskge3(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, T a
     RBH_HIP(st.map(A, sizeof(T) * extent(layout, rows_A, cols_A, lda), true, false, &dA));
     RBH_HIP(st.map_out(B, sizeof(T), layout, d, n, ldb, beta != (T)0, &dB));
     RBH_HIP(st.map(S_buff, sizeof(T) * D->n_rows * D->n_cols, true, false, &dS));
-
     GemmProblem p{};
+    build_left<T>(p, layout, opS, opA, d, n, m, alpha, beta, D, seed, dS, S_layout, ro_s, co_s, dA, lda, dB, ldb);
+    int rc = run_dense<T>(p, s);
+    if (rc) return rc;
+    RBH_HIP(st.finish());
+    return RBH_OK;
+}
+
+// The canonical problem of a left sketch B = alpha op(submat(S)) op(A) + beta B on device pointers
+// (dS == NULL: the operator is generated).
+template <typename T>
+void build_left(GemmProblem &p, char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, T alpha, T beta,
+                const rbh_dense_dist *D, const rbh_state *seed, const void *dS, char S_layout, int64_t ro_s,
+                int64_t co_s, const void *dA, int64_t lda, void *dB, int64_t ldb) {
     p.alpha = alpha;
     p.beta = beta;
     p.C = dB;
@@ -361,10 +403,6 @@ int lskge3(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, T a
     }
     p.xmode = p.xkind == MEM ? mem_mode<T>(p.xm.ptr, p.xm.so, p.xm.sk, p.K) : 0;
     p.ymode = p.ykind == MEM ? mem_mode<T>(p.ym.ptr, p.ym.so, p.ym.sk, p.K) : 0;
-    int rc = run_dense<T>(p, s);
-    if (rc) return rc;
-    RBH_HIP(st.finish());
-    return RBH_OK;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -403,8 +441,19 @@ int rskge3(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, T a
     RBH_HIP(st.map(A, sizeof(T) * extent(layout, rows_A, cols_A, lda), true, false, &dA));
     RBH_HIP(st.map_out(B, sizeof(T), layout, m, d, ldb, beta != (T)0, &dB));
     RBH_HIP(st.map(S_buff, sizeof(T) * D->n_rows * D->n_cols, true, false, &dS));
-
     GemmProblem p{};
+    build_right<T>(p, layout, opA, opS, m, d, n, alpha, beta, dA, lda, D, seed, dS, S_layout, ro_s, co_s, dB, ldb);
+    int rc = run_dense<T>(p, s);
+    if (rc) return rc;
+    RBH_HIP(st.finish());
+    return RBH_OK;
+}
+
+// The canonical problem of a right sketch B = alpha op(A) op(submat(S)) + beta B on device pointers.
+template <typename T>
+void build_right(GemmProblem &p, char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, T alpha, T beta,
+                 const void *dA, int64_t lda, const rbh_dense_dist *D, const rbh_state *seed, const void *dS,
+                 char S_layout, int64_t ro_s, int64_t co_s, void *dB, int64_t ldb) {
     p.alpha = alpha;
     p.beta = beta;
     p.C = dB;
@@ -440,10 +489,6 @@ int rskge3(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, T a
     }
     p.xmode = p.xkind == MEM ? mem_mode<T>(p.xm.ptr, p.xm.so, p.xm.sk, p.K) : 0;
     p.ymode = p.ykind == MEM ? mem_mode<T>(p.ym.ptr, p.ym.so, p.ym.sk, p.K) : 0;
-    int rc = run_dense<T>(p, s);
-    if (rc) return rc;
-    RBH_HIP(st.finish());
-    return RBH_OK;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -933,6 +978,21 @@ template <> hipError_t launch_sym_t<float>(char l, const float *A, int64_t n, in
     return launch_symcheck_f32(l, A, n, lda, tol, f, s);
 }
 
+// The device check on a device pointer: *flags bit 0 = the reference's predicate failed somewhere,
+// bit 1 = some mirrored pair is not bitwise equal. Synchronises the stream (the caller must know).
+template <typename T>
+int symcheck_flags(char layout, const T *dA, int64_t n, int64_t lda, T tol, hipStream_t s, int *flags) {
+    *flags = 0;
+    int *flag = nullptr;
+    RBH_HIP(ws_alloc((void **)&flag, sizeof(int), s));
+    RBH_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
+    RBH_HIP(launch_sym_t<T>(layout, dA, n, lda, tol, flag, s));
+    RBH_HIP(hipMemcpyAsync(flags, flag, sizeof(int), hipMemcpyDeviceToHost, s));
+    RBH_HIP(ws_free(flag, s));
+    RBH_HIP(hipStreamSynchronize(s));
+    return RBH_OK;
+}
+
 template <typename T>
 int require_symmetric(char layout, const T *A, int64_t n, int64_t lda, T tol, void *stream) {
     if (tol < 0) return RBH_OK;   // util.hh:166-168
@@ -942,16 +1002,153 @@ int require_symmetric(char layout, const T *A, int64_t n, int64_t lda, T tol, vo
     Stager st(s);
     void *dA;
     RBH_HIP(st.map(A, sizeof(T) * extent(layout, n, n, lda), true, false, &dA));
-    int *flag = nullptr;
-    RBH_HIP(ws_alloc((void **)&flag, sizeof(int), s));
-    RBH_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
-    RBH_HIP(launch_sym_t<T>(layout, (const T *)dA, n, lda, tol, flag, s));
     int h = 0;
-    RBH_HIP(hipMemcpyAsync(&h, flag, sizeof(int), hipMemcpyDeviceToHost, s));
-    RBH_HIP(ws_free(flag, s));
-    RBH_HIP(hipStreamSynchronize(s));
+    int rc = symcheck_flags<T>(layout, (const T *)dA, n, lda, tol, s, &h);
+    if (rc) return rc;
     RBH_HIP(st.finish());
-    if (h) return set_error(RBH_ERR_SYMMETRY, "Symmetry check failed, in function require_symmetric");
+    if (h & 1) return set_error(RBH_ERR_SYMMETRY, "Symmetry check failed, in function require_symmetric");
+    return RBH_OK;
+}
+
+template <typename T> hipError_t launch_symz_t(int, const T *, int64_t, int64_t, T *, hipStream_t);
+template <> hipError_t launch_symz_t<double>(int t, const double *A, int64_t lda, int64_t n, double *o, hipStream_t s) {
+    return launch_symmetrize_f64(t, A, lda, n, o, s);
+}
+template <> hipError_t launch_symz_t<float>(int t, const float *A, int64_t lda, int64_t n, float *o, hipStream_t s) {
+    return launch_symmetrize_f32(t, A, lda, n, o, s);
+}
+
+// Symmetric sketch reading one triangle of A (device pointers): side 'L' B (d x n) =
+// alpha submat(S) A + beta B, side 'R' B (n x d) = alpha A submat(S) + beta B. A symmetric n x n in
+// `layout`: fmt 'F' full storage (lda), only triangle `uplo` read; fmt 'P' that triangle packed.
+// The fused one-triangle kernel runs when it applies (skge_dense.hip); otherwise the triangle is
+// expanded into a workspace and the plain kernels run.
+template <typename T>
+int sksy_tri_dev(char layout, char side, char uplo, char fmt, int64_t d, int64_t n, T alpha, const rbh_dense_dist *D,
+                 const rbh_state *seed, const void *dS, char S_layout, int64_t ro_s, int64_t co_s, const void *dA,
+                 int64_t lda, T beta, void *dB, int64_t ldb, hipStream_t s) {
+    GemmProblem p{};
+    const int64_t lda_eff = fmt == 'F' ? lda : n;
+    if (side == 'L') build_left<T>(p, layout, 'N', 'N', d, n, n, alpha, beta, D, seed, dS, S_layout, ro_s, co_s, dA,
+                                   lda_eff, dB, ldb);
+    else build_right<T>(p, layout, 'N', 'N', n, d, n, alpha, beta, dA, lda_eff, D, seed, dS, S_layout, ro_s, co_s, dB,
+                        ldb);
+    if (p.M <= 0 || p.N <= 0) return RBH_OK;
+    // A as the operand (o, k) -> storage o*lda + k, valid for every layout by symmetry
+    const bool a_is_x = side == 'L' ? layout == 'R' : layout == 'C';
+    MemOperand &mo = a_is_x ? p.xm : p.ym;
+    int &mode = a_is_x ? p.xmode : p.ymode;
+    mo.ptr = dA;
+    mo.so = lda_eff;
+    mo.sk = 1;
+    mode = mem_mode<T>(mo.ptr, mo.so, mo.sk, p.K);
+    const bool kle = (layout == 'C') == (uplo == 'U');   // (o, k) stored when k <= o
+    p.tri = (kle ? 1 : 2) + (fmt == 'P' ? 2 : 0);
+    p.tri_n = n;
+    if (p.K <= 0 || p.alpha == 0.0) { p.tri = 0; return run_dense<T>(p, s); }
+    hipError_t e = launch_gemm_t<T>(p, s);
+    if (e == hipSuccess) return RBH_OK;
+    if (e != hipErrorNotSupported) RBH_HIP(e);
+    (void)hipGetLastError();
+    void *full = nullptr;
+    RBH_HIP(ws_alloc(&full, sizeof(T) * (size_t)n * (size_t)n, s));
+    RBH_HIP(launch_symz_t<T>(p.tri, (const T *)dA, lda_eff, n, (T *)full, s));
+    mo.ptr = full;
+    mo.so = n;
+    mode = mem_mode<T>(mo.ptr, mo.so, mo.sk, p.K);
+    p.tri = 0;
+    int rc = run_dense<T>(p, s);
+    RBH_HIP(ws_free(full, s));
+    return rc;
+}
+
+// the argument checks shared by the symmetric entry points (sksy.hh's sketch_general calls:
+// skge.hh:197-206 / 346-355 with m = n and the window checks of the operator)
+int check_sksy(char layout, char side, int64_t d, int64_t n, const rbh_dense_dist *D, const rbh_state *seed,
+               const void *S_buff, char S_layout, int64_t ro_s, int64_t co_s, int64_t ldb) {
+    RBH_REQUIRE(layout == 'C' || layout == 'R');
+    RBH_REQUIRE(side == 'L' || side == 'R');
+    RBH_REQUIRE(D != nullptr);
+    RBH_REQUIRE(d >= 0 && n >= 0 && ro_s >= 0 && co_s >= 0);
+    const int64_t sr = side == 'L' ? d : n, sc = side == 'L' ? n : d;
+    RBH_REQUIRE(D->n_rows >= sr + ro_s);
+    RBH_REQUIRE(D->n_cols >= sc + co_s);
+    const int64_t br = side == 'L' ? d : n, bc = side == 'L' ? n : d;
+    if (layout == 'C') RBH_REQUIRE(ldb >= br);
+    else RBH_REQUIRE(ldb >= bc);
+    if (!S_buff) {
+        RBH_REQUIRE(seed != nullptr);
+        RBH_REQUIRE(D->family != 'B');
+        RBH_REQUIRE(D->major_axis != 'U');
+    } else {
+        RBH_REQUIRE(S_layout == 'C' || S_layout == 'R');
+    }
+    return RBH_OK;
+}
+
+// sksy extension: one triangle (full storage or packed) of a symmetric A
+template <typename T>
+int sksy_tri(char layout, char side, char uplo, char fmt, int64_t d, int64_t n, T alpha, const rbh_dense_dist *D,
+             const rbh_state *seed, const T *S_buff, char S_layout, int64_t ro_s, int64_t co_s, const T *A, int64_t lda,
+             T beta, T *B, int64_t ldb, void *stream) {
+    int rc = check_sksy(layout, side, d, n, D, seed, S_buff, S_layout, ro_s, co_s, ldb);
+    if (rc) return rc;
+    RBH_REQUIRE(uplo == 'U' || uplo == 'L');
+    RBH_REQUIRE(fmt == 'F' || fmt == 'P');
+    if (fmt == 'F') RBH_REQUIRE(lda >= n);
+    hipStream_t s = (hipStream_t)stream;
+    Stager st(s);
+    void *dA, *dB, *dS;
+    const int64_t a_elems = fmt == 'F' ? extent(layout, n, n, lda) : n * (n + 1) / 2;
+    RBH_HIP(st.map(A, sizeof(T) * a_elems, true, false, &dA));
+    RBH_HIP(st.map_out(B, sizeof(T), layout, side == 'L' ? d : n, side == 'L' ? n : d, ldb, beta != (T)0, &dB));
+    RBH_HIP(st.map(S_buff, sizeof(T) * D->n_rows * D->n_cols, true, false, &dS));
+    rc = sksy_tri_dev<T>(layout, side, uplo, fmt, d, n, alpha, D, seed, dS, S_layout, ro_s, co_s, dA, lda, beta, dB,
+                         ldb, s);
+    if (rc) return rc;
+    RBH_HIP(st.finish());
+    return RBH_OK;
+}
+
+// sketch_symmetric (sksy.hh:165-537) in one call: util::require_symmetric with tol (skipped when
+// tol < 0, util.hh:166-168), then sketch_general on full storage. With RBH_SKSY_TRI=1, and when the
+// check ran and found A bitwise symmetric, only the upper triangle is read instead: the operand
+// tiles are then identical, so the result is the full-storage product's bit for bit. It is not the
+// default: every stored tile is then fetched twice (once per role), so the fabric traffic is the
+// same, and the mirror / diagonal tiles cost 4.5 % at C5.
+template <typename T>
+int sketch_symmetric(char layout, char side, int64_t d, int64_t n, T alpha, const rbh_dense_dist *D,
+                     const rbh_state *seed, const T *S_buff, char S_layout, int64_t ro_s, int64_t co_s, const T *A,
+                     int64_t lda, T beta, T *B, int64_t ldb, T tol, void *stream) {
+    int rc = check_sksy(layout, side, d, n, D, seed, S_buff, S_layout, ro_s, co_s, ldb);
+    if (rc) return rc;
+    RBH_REQUIRE(lda >= n);
+    hipStream_t s = (hipStream_t)stream;
+    Stager st(s);
+    void *dA, *dB, *dS;
+    RBH_HIP(st.map(A, sizeof(T) * extent(layout, n, n, lda), true, false, &dA));
+    int flags = 2;   // unchecked: read both triangles
+    if (tol >= 0) {
+        rc = symcheck_flags<T>(layout, (const T *)dA, n, lda, tol, s, &flags);
+        if (rc) return rc;
+        if (flags & 1) return set_error(RBH_ERR_SYMMETRY, "Symmetry check failed, in function require_symmetric");
+    }
+    RBH_HIP(st.map_out(B, sizeof(T), layout, side == 'L' ? d : n, side == 'L' ? n : d, ldb, beta != (T)0, &dB));
+    RBH_HIP(st.map(S_buff, sizeof(T) * D->n_rows * D->n_cols, true, false, &dS));
+    static const bool use_tri = [] { const char *e = getenv("RBH_SKSY_TRI"); return e && e[0] == '1'; }();
+    if (!(flags & 2) && use_tri) {
+        rc = sksy_tri_dev<T>(layout, side, 'U', 'F', d, n, alpha, D, seed, dS, S_layout, ro_s, co_s, dA, lda, beta,
+                             dB, ldb, s);
+    } else {
+        GemmProblem p{};
+        if (side == 'L') build_left<T>(p, layout, 'N', 'N', d, n, n, alpha, beta, D, seed, dS, S_layout, ro_s, co_s,
+                                       dA, lda, dB, ldb);
+        else build_right<T>(p, layout, 'N', 'N', n, d, n, alpha, beta, dA, lda, D, seed, dS, S_layout, ro_s, co_s, dB,
+                            ldb);
+        rc = run_dense<T>(p, s);
+    }
+    if (rc) return rc;
+    RBH_HIP(st.finish());
     return RBH_OK;
 }
 
@@ -1139,6 +1336,33 @@ int rbh_spmm_right_f32(char layout, char opA, char opB, int64_t m, int64_t n, in
     if (opB != 'N' && opB != 'T') return set_error(RBH_ERR_REQUIRE, "(opB is NoTrans or Trans) was required, but did not hold, in function right_spmm");
     return spmm_left<float>(layout == 'C' ? 'R' : 'C', opB == 'N' ? 'T' : 'N', opA, n, m, k, alpha, B_fmt, B_rows,
                             B_cols, B_nnz, B_p, B_i, B_v, ro_b, co_b, A, lda, beta, C, ldc, stream);
+}
+
+int rbh_sketch_symmetric_f64(char layout, char side, int64_t d, int64_t n, double alpha, const rbh_dense_dist *D,
+                             const rbh_state *seed, const double *S_buff, char S_layout, int64_t ro_s, int64_t co_s,
+                             const double *A, int64_t lda, double beta, double *B, int64_t ldb, double sym_check_tol,
+                             void *stream) {
+    return sketch_symmetric<double>(layout, side, d, n, alpha, D, seed, S_buff, S_layout, ro_s, co_s, A, lda, beta, B,
+                                    ldb, sym_check_tol, stream);
+}
+int rbh_sketch_symmetric_f32(char layout, char side, int64_t d, int64_t n, float alpha, const rbh_dense_dist *D,
+                             const rbh_state *seed, const float *S_buff, char S_layout, int64_t ro_s, int64_t co_s,
+                             const float *A, int64_t lda, float beta, float *B, int64_t ldb, float sym_check_tol,
+                             void *stream) {
+    return sketch_symmetric<float>(layout, side, d, n, alpha, D, seed, S_buff, S_layout, ro_s, co_s, A, lda, beta, B,
+                                   ldb, sym_check_tol, stream);
+}
+int rbh_sksy_tri_f64(char layout, char side, char uplo, char A_fmt, int64_t d, int64_t n, double alpha,
+                     const rbh_dense_dist *D, const rbh_state *seed, const double *S_buff, char S_layout, int64_t ro_s,
+                     int64_t co_s, const double *A, int64_t lda, double beta, double *B, int64_t ldb, void *stream) {
+    return sksy_tri<double>(layout, side, uplo, A_fmt, d, n, alpha, D, seed, S_buff, S_layout, ro_s, co_s, A, lda, beta,
+                            B, ldb, stream);
+}
+int rbh_sksy_tri_f32(char layout, char side, char uplo, char A_fmt, int64_t d, int64_t n, float alpha,
+                     const rbh_dense_dist *D, const rbh_state *seed, const float *S_buff, char S_layout, int64_t ro_s,
+                     int64_t co_s, const float *A, int64_t lda, float beta, float *B, int64_t ldb, void *stream) {
+    return sksy_tri<float>(layout, side, uplo, A_fmt, d, n, alpha, D, seed, S_buff, S_layout, ro_s, co_s, A, lda, beta,
+                           B, ldb, stream);
 }
 
 int rbh_require_symmetric_f64(char layout, const double *A, int64_t n, int64_t lda, double tol, void *stream) {

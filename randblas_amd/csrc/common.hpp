@@ -49,7 +49,17 @@ struct GemmProblem {
     GenOperand xg, yg;
     int splitk;          // > 1: the fused kernel splits K; workgroup z writes alpha * its partial sum
     void *partial;       //      to partial[z] (M x N col-major), and a reduction forms C
+    // One-triangle symmetric memory operand (sketch_symmetric): 0 = plain. Otherwise element
+    // (o, k) is stored only where k <= o (1 full storage ptr[o*so + k], 3 packed ptr[k + o(o+1)/2])
+    // or k >= o (2 full, 4 packed ptr[(k - o) + o*tri_n - o(o-1)/2]); the rest is its mirror (k, o).
+    int tri;
+    int64_t tri_n;
 };
+
+// Expand a one-triangle operand (GemmProblem::tri conventions, n x n) into full storage
+// out[o*n + k] (skge_dense.hip); the fallback when the fused one-triangle kernel does not apply.
+hipError_t launch_symmetrize_f64(int tri, const double *A, int64_t lda, int64_t n, double *out, hipStream_t s);
+hipError_t launch_symmetrize_f32(int tri, const float *A, int64_t lda, int64_t n, float *out, hipStream_t s);
 
 // Kernel launchers (skge_dense.hip)
 hipError_t launch_gemm_f64(const GemmProblem &p, hipStream_t s);

@@ -536,7 +536,13 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 #ifndef RBH_WIDE_WG
 #define RBH_WIDE_WG 1
 #endif
-template <int GK, int FAMILY, bool GX>
+// TRI != 0: the memory operand is a symmetric matrix of which only one triangle is read
+// (sketch_symmetric, sksy.hh:165-537, with A's other triangle never touched). In the operand's own
+// coordinates (o, k) the stored triangle is k <= o (TRI 1 full storage, 3 packed) or k >= o (2, 4);
+// element (o, k) outside it is the stored (k, o). A K step's 512 x 16 tile is then wholly inside
+// the triangle (loaded as usual), wholly outside (loaded from the mirror tile, which is contiguous
+// along o, and transposed into the LDS image), or straddles the diagonal (per-element select).
+template <int GK, int FAMILY, bool GX, int TRI = 0>
 __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
     typedef double T;
     // 8 waves = WGW (along the generated dimension) x WMW (along the memory dimension); each wave
@@ -612,6 +618,82 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) *reinterpret_cast<v2_t *>(dst + 1024 * (4 * half + e)) = rs[e];
     };
+    // ---- one-triangle memory operand (TRI != 0) ----
+    constexpr bool TKLE = TRI == 1 || TRI == 3, TPACK = TRI >= 3;
+    const bool mfull = mo0 + BMM <= mnO;
+    // stored element (a, b) of the triangle (b <= a for TKLE, b >= a otherwise); 32-bit index
+    // arithmetic (the launcher checks that every index fits in 31 bits)
+    const uint32_t tso = (uint32_t)mop.so, tn = (uint32_t)p.tri_n;
+    auto sidx = [&](uint32_t a, uint32_t b) -> uint32_t {
+        if (TRI == 3) return b + a * (a + 1) / 2;
+        if (TRI == 4) return (b - a) + a * tn - a * (a - 1) / 2;
+        return a * tso + b;
+    };
+    auto eidx = [&](uint32_t o, uint32_t k) -> uint32_t {
+        const bool in = TKLE ? k <= o : k >= o;
+        return in ? sidx(o, k) : sidx(k, o);
+    };
+    // step class: 0 inside the triangle, 1 mirrored, 2 straddles the diagonal (or a partial tile)
+    auto tclass = [&](int64_t k0) -> int {
+        if (TRI == 0) return 0;
+        if (!mfull) return 2;
+        if (TKLE) return k0 + BK - 1 <= mo0 ? 0 : (k0 >= mo0 + BMM ? 1 : 2);
+        return k0 >= mo0 + BMM - 1 ? 0 : (k0 + BK - 1 < mo0 ? 1 : 2);
+    };
+    auto rload_tri = [&](int64_t k0, int half, int cls) {
+        const int64_t ck0 = k0 < p.K ? k0 : p.K - BK;
+        if (cls == 0 && !TPACK) { rload(k0, half); return; }
+        if (cls == 1) {
+            // mirror: a 2 x 2 block per load pair -- (o, o + 1) at k and at k + 1, stored at (k, o..o+1)
+            // and (k + 1, o..o+1) -- transposed in registers by rstore_tri into the usual 16-B slots
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const uint32_t k = (uint32_t)ck0 + 2 * ((tid >> 8) + 2 * (2 * half + e)), o = (uint32_t)mo0 + 2 * (tid & 255);
+                const uint32_t i0 = sidx(k, o), i1 = sidx(k + 1, o);
+                if (!TPACK) {
+                    rs[2 * e] = *reinterpret_cast<const v2_t *>(mptr + i0);
+                    rs[2 * e + 1] = *reinterpret_cast<const v2_t *>(mptr + i1);
+                } else {
+                    rs[2 * e][0] = mptr[i0];
+                    rs[2 * e][1] = mptr[i0 + 1];
+                    rs[2 * e + 1][0] = mptr[i1];
+                    rs[2 * e + 1][1] = mptr[i1 + 1];
+                }
+            }
+            return;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            uint32_t ia, ib;   // the vector's two elements, consecutive in storage for class 0
+            {                  // (o, k) and (o, k + 1) of the usual image
+                int64_t o64 = mo0 + (tid >> 3) + 64 * (4 * half + e);
+                const uint32_t o = (uint32_t)(o64 < mnO ? o64 : mnO - 1);
+                const uint32_t k = (uint32_t)ck0 + 2 * (tid & 7);
+                if (cls == 0) { ia = sidx(o, k); ib = ia + 1; }
+                else { ia = eidx(o, k); ib = eidx(o, k + 1); }
+            }
+            rs[e][0] = mptr[ia];
+            rs[e][1] = mptr[ib];
+        }
+    };
+    auto rstore_tri = [&](int st, int half, int cls) {
+        if (cls != 1) { rstore(st, half); return; }
+        // mirror pairs: rows o = 2 op and o + 1 of the image get (k, k + 1) in 16-B slot k/2, which
+        // rows o and o + 1 swizzle alike ((o >> 1) & 7 = op & 7); 8 lanes of a 16-B store group
+        // hit 8 distinct slots
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int kp = (tid >> 8) + 2 * (2 * half + e), op = tid & 255;
+            T *dst = lds + st * MS + 2 * op * BK + 2 * (kp ^ (op & 7));
+            v2_t r0, r1;
+            r0[0] = rs[2 * e][0];
+            r0[1] = rs[2 * e + 1][0];
+            r1[0] = rs[2 * e][1];
+            r1[1] = rs[2 * e + 1][1];
+            *reinterpret_cast<v2_t *>(dst) = r0;
+            *reinterpret_cast<v2_t *>(dst + BK) = r1;
+        }
+    };
     // draw of the 64 x 16 generated tile for step kt (waves 0-3, one Philox call per lane). (A
     // counter precomputed per lane, advanced by a uniform step, saves a few VALU but costs the
     // 4 VGPRs this kernel does not have.)
@@ -673,7 +755,12 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
     const int64_t nk = p.K / BK;
     __syncthreads();   // tab
 #ifndef RBH_WIDE_DMA
-    rload(0, 0); rstore(0, 0); rload(0, 1); rstore(0, 1);
+    if (TRI) {
+        const int c0 = tclass(0);
+        rload_tri(0, 0, c0); rstore_tri(0, 0, c0); rload_tri(0, 1, c0); rstore_tri(0, 1, c0);
+    } else {
+        rload(0, 0); rstore(0, 0); rload(0, 1); rstore(0, 1);
+    }
 #else
     dma(0, 0);
 #endif
@@ -689,8 +776,10 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
         const T *Mc = lds + cur * MS;
         const T *Gc = lds + 2 * MS + cur * GS;
         const int64_t kn = (kt + 1) * BK;
+        const int cn = tclass(kn);
 #ifndef RBH_WIDE_DMA
-        rload(kn, 0);
+        if (TRI) rload_tri(kn, 0, cn);
+        else rload(kn, 0);
 #else
         dma(kn, cur ^ 1);
 #endif
@@ -698,7 +787,10 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
 #ifndef RBH_WIDE_DMA
-            if (s == 2) { rstore(cur ^ 1, 0); rload(kn, 1); }
+            if (s == 2) {
+                if (TRI) { rstore_tri(cur ^ 1, 0, cn); rload_tri(kn, 1, cn); }
+                else { rstore(cur ^ 1, 0); rload(kn, 1); }
+            }
 #endif
             T gf[FA];
 #pragma unroll
@@ -718,7 +810,8 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
         }
         if (wave < 4) gstore(cur ^ 1);
 #ifndef RBH_WIDE_DMA
-        rstore(cur ^ 1, 1);
+        if (TRI) rstore_tri(cur ^ 1, 1, cn);
+        else rstore(cur ^ 1, 1);
 #endif
         __syncthreads();
     }
@@ -831,13 +924,13 @@ static bool fused_ok(const GemmProblem &p) {
     return mode == 2 && (g.pc0 & 3) == 0;
 }
 
-template <int GK, int FAMILY, bool GX>
+template <int GK, int FAMILY, bool GX, int TRI = 0>
 static hipError_t launch_wide(const GemmProblem &p, hipStream_t s) {
     const int64_t gnO = GX ? p.M : p.N, mnO = GX ? p.N : p.M;
     const int64_t nb = ((gnO + 63) / 64) * ((mnO + 511) / 512);
     if (nb <= 0) return hipSuccess;
     timing_begin(s);
-    hipLaunchKernelGGL((skge_wide_kernel<GK, FAMILY, GX>), dim3((unsigned)nb), dim3(512), 0, s, p);
+    hipLaunchKernelGGL((skge_wide_kernel<GK, FAMILY, GX, TRI>), dim3((unsigned)nb), dim3(512), 0, s, p);
     hipError_t e = hipGetLastError();
     timing_end(s);
     return e;
@@ -849,8 +942,40 @@ static bool wide_ok(const GemmProblem &p) {
     return sizeof(T) == 8 && !off && fused_ok(p) && p.K % BK == 0;
 }
 
+// One-triangle symmetric memory operand: the wide f64 kernel when the generated operand runs its
+// counter along k from a Philox quad (GEN_OK, every MajorAxis::Long operator) and K % 16 == 0; full
+// storage also needs 16-B aligned rows. Otherwise hipErrorNotSupported, and the caller expands
+// the triangle (launch_symmetrize) and runs the plain kernels.
+template <int FAM, bool GX>
+static hipError_t launch_wide_tri(const GemmProblem &p, hipStream_t s) {
+    switch (p.tri) {
+    case 1: return launch_wide<GEN_OK, FAM, GX, 1>(p, s);
+    case 2: return launch_wide<GEN_OK, FAM, GX, 2>(p, s);
+    case 3: return launch_wide<GEN_OK, FAM, GX, 3>(p, s);
+    case 4: return launch_wide<GEN_OK, FAM, GX, 4>(p, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+template <typename T>
+static hipError_t launch_gemm_tri(const GemmProblem &p, hipStream_t s) {
+    if (sizeof(T) != 8 || (p.xkind == MEM) == (p.ykind == MEM)) return hipErrorNotSupported;
+    const bool gx = p.xkind != MEM;
+    const GenOperand &g = gx ? p.xg : p.yg;
+    const MemOperand &m = gx ? p.ym : p.xm;
+    if ((gx ? p.xkind : p.ykind) != GEN_OK || (g.pc0 & 3) || p.K % BK) return hipErrorNotSupported;
+    if (p.tri <= 2 && ((((uintptr_t)m.ptr) % 16) || (m.so & 1))) return hipErrorNotSupported;
+    // 31-bit element indices in the kernel
+    const int64_t n = p.tri_n, last = p.tri <= 2 ? (n - 1) * m.so + n : n * (n + 1) / 2;
+    if (last >= ((int64_t)1 << 31)) return hipErrorNotSupported;
+    const bool unif = g.family == rb::UNIFORM;
+    if (gx) return unif ? launch_wide_tri<rb::UNIFORM, true>(p, s) : launch_wide_tri<rb::GAUSSIAN, true>(p, s);
+    return unif ? launch_wide_tri<rb::UNIFORM, false>(p, s) : launch_wide_tri<rb::GAUSSIAN, false>(p, s);
+}
+
 template <typename T>
 static hipError_t launch_gemm(const GemmProblem &p, hipStream_t s) {
+    if (p.tri) return launch_gemm_tri<T>(p, s);
     const bool unif = (p.xkind != MEM ? p.xg.family : p.yg.family) == rb::UNIFORM;
     if (wide_ok<T>(p)) {
 #define RBH_WIDE_L(GK, GX)                                                                     \
@@ -900,6 +1025,38 @@ static hipError_t launch_gemm(const GemmProblem &p, hipStream_t s) {
 
 hipError_t launch_gemm_f64(const GemmProblem &p, hipStream_t s) { return launch_gemm<double>(p, s); }
 hipError_t launch_gemm_f32(const GemmProblem &p, hipStream_t s) { return launch_gemm<float>(p, s); }
+
+// out[o*n + k] = operand element (o, k) of a one-triangle symmetric matrix (GemmProblem::tri)
+template <typename T>
+__global__ void symmetrize_kernel(int tri, const T *A, int64_t lda, int64_t n, T *out) {
+    const int64_t total = n * n;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t o = e / n, k = e % n;
+        const bool kle = tri == 1 || tri == 3;
+        const bool in = kle ? k <= o : k >= o;
+        const int64_t a = in ? o : k, b = in ? k : o;
+        int64_t idx;
+        if (tri == 3) idx = b + a * (a + 1) / 2;
+        else if (tri == 4) idx = (b - a) + a * n - a * (a - 1) / 2;
+        else idx = a * lda + b;
+        out[e] = A[idx];
+    }
+}
+
+template <typename T>
+static hipError_t launch_symmetrize(int tri, const T *A, int64_t lda, int64_t n, T *out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    int64_t blocks = (n * n + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(symmetrize_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, s, tri, A, lda, n, out);
+    return hipGetLastError();
+}
+hipError_t launch_symmetrize_f64(int tri, const double *A, int64_t lda, int64_t n, double *out, hipStream_t s) {
+    return launch_symmetrize<double>(tri, A, lda, n, out, s);
+}
+hipError_t launch_symmetrize_f32(int tri, const float *A, int64_t lda, int64_t n, float *out, hipStream_t s) {
+    return launch_symmetrize<float>(tri, A, lda, n, out, s);
+}
 
 template <typename T>
 static hipError_t launch_scale(int64_t M, int64_t N, T beta, T *C, int64_t ldc, hipStream_t s) {

@@ -4,7 +4,8 @@
 // One workgroup compares a 64 x 64 tile of the strict upper block triangle with its mirror: the
 // mirror tile is read coalesced and transposed through LDS, so A is read once at streaming rate.
 // The predicate is the reference's, in the operand precision T:
-//   viol = |A(i,j) - A(j,i)| > (|A(i,j)| + |A(j,i)| + 1) * tol.
+//   viol = |A(i,j) - A(j,i)| > (|A(i,j)| + |A(j,i)| + 1) * tol   -> flag bit 0;
+// bit 1 marks a pair whose bits differ (sketch_symmetric then reads both triangles).
 #include "saso.hpp"
 
 namespace rbh {
@@ -13,38 +14,63 @@ template <typename T>
 __global__ __launch_bounds__(256) void symcheck_kernel(int64_t n, const T *A, int64_t irs, int64_t ics, T tol,
                                                        int *flag) {
     __shared__ T mir[64][65];
-    // blockIdx.x enumerates tile pairs (bi <= bj) row by row of the upper block triangle
+    // blockIdx.x enumerates tile pairs (bi <= bj) row by row of the upper block triangle: block b of
+    // block-row bi starts at bi*nt - bi(bi-1)/2; bi from the quadratic, then a one-step fix-up
     const int64_t nt = (n + 63) / 64;
-    int64_t b = blockIdx.x, bi = 0;
-    while (b >= nt - bi) { b -= nt - bi; ++bi; }
-    const int64_t bj = bi + b;
+    const int64_t b0 = blockIdx.x;
+    const double tt = 2.0 * (double)nt + 1.0;
+    int64_t bi = (int64_t)((tt - sqrt(tt * tt - 8.0 * (double)b0)) * 0.5);
+    auto rstart = [&](int64_t r) { return r * nt - r * (r - 1) / 2; };
+    while (bi > 0 && rstart(bi) > b0) --bi;
+    while (rstart(bi + 1) <= b0) ++bi;
+    const int64_t bj = bi + (b0 - rstart(bi));
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;   // 64 x 4
-    // mirror tile: A(bj*64 + r, bi*64 + c), stored transposed as mir[c][r]
-    for (int rr = ty; rr < 64; rr += 4) {
-        // coalesce along whichever index is contiguous
+    // both tiles' loads are issued before any is used: the mirror tile A(bj*64 + r, bi*64 + c) and
+    // this tile A(bi*64 + r, bj*64 + c), 16 rows each per thread, coalesced along the contiguous index
+    T mv[16], av[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int rr = ty + 4 * q;
         int64_t gi, gj;
-        int lr, lc;
-        if (irs == 1) { gi = bj * 64 + tx; gj = bi * 64 + rr; lr = tx; lc = rr; }
-        else { gi = bj * 64 + rr; gj = bi * 64 + tx; lr = rr; lc = tx; }
-        mir[lc][lr] = (gi < n && gj < n) ? A[gi * irs + gj * ics] : (T)0;
+        if (irs == 1) { gi = bj * 64 + tx; gj = bi * 64 + rr; }
+        else { gi = bj * 64 + rr; gj = bi * 64 + tx; }
+        mv[q] = (gi < n && gj < n) ? A[gi * irs + gj * ics] : (T)0;
+        if (irs == 1) { gi = bi * 64 + tx; gj = bj * 64 + rr; }
+        else { gi = bi * 64 + rr; gj = bj * 64 + tx; }
+        av[q] = (gi < n && gj < n) ? A[gi * irs + gj * ics] : (T)0;
+    }
+    // mirror tile stored transposed: mir[c][r] = A(bj*64 + r, bi*64 + c)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int rr = ty + 4 * q;
+        if (irs == 1) mir[rr][tx] = mv[q];
+        else mir[tx][rr] = mv[q];
     }
     __syncthreads();
-    bool bad = false;
-    for (int rr = ty; rr < 64; rr += 4) {
+    bool bad = false, bitdiff = false;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int rr = ty + 4 * q;
         int64_t gi, gj;
         int lr, lc;
         if (irs == 1) { gi = bi * 64 + tx; gj = bj * 64 + rr; lr = tx; lc = rr; }
         else { gi = bi * 64 + rr; gj = bj * 64 + tx; lr = rr; lc = tx; }
         if (gi < n && gj < n && gi < gj) {
-            const T aij = A[gi * irs + gj * ics];
+            const T aij = av[q];
             const T aji = mir[lr][lc];   // A(gj, gi)
             const T d = aij - aji;
             const T viol = d < (T)0 ? -d : d;
             const T rel = ((aij < (T)0 ? -aij : aij) + (aji < (T)0 ? -aji : aji) + (T)1) * tol;
             if (viol > rel) bad = true;
+            // not bitwise symmetric (a passing check can still hide NaNs or signed zeros): then a
+            // one-triangle read would not reproduce the full-storage product exactly
+            if (sizeof(T) == 8 ? __double_as_longlong((double)aij) != __double_as_longlong((double)aji)
+                               : __float_as_uint((float)aij) != __float_as_uint((float)aji))
+                bitdiff = true;
         }
     }
-    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+    const int f = (__any(bad) ? 1 : 0) | (__any(bitdiff) ? 2 : 0);
+    if (f && (threadIdx.x & 63) == 0) atomicOr(flag, f);
 }
 
 template <typename T>

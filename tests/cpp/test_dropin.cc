@@ -324,6 +324,8 @@ static void sparse_operator_state() {
     std::vector<int64_t> r0(S.rows, S.rows + nnz);
     RandBLAS::sketch_general(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, m, 1.0, S, A.data(), m, 0.0, B2.data(), d);
     for (int64_t e = 0; e < d * n; ++e) CHECK(B2[e] == B[e]);
+    if (std::getenv("RBH_DIAG"))
+        for (int64_t e = 0; e < 8; ++e) std::printf("diag B[%ld] = %.17g  B2 = %.17g\n", (long)e, B[e], B2[e]);
     for (int64_t e = 0; e < nnz; ++e) CHECK(S.rows[e] == r0[e]);
     // opS = Trans on an unfilled operator: the view is transposed, arrays end sorted by (row, col)
     RandBLAS::SparseSkOp<double> T(RandBLAS::SparseDist{m, d, 3}, 12);
@@ -401,6 +403,28 @@ static void spmm_both_sides() {
     CHECK(threw);
 }
 
+// sketch_symmetric reads one triangle of a bitwise-symmetric A: the same bits as sketch_general on
+// all of A; the packed-storage extension gives the same bits again.
+static void symmetric_one_triangle() {
+    const int64_t n = 160, d = 32;
+    auto M = random_matrix<double>(n, n, 21);
+    std::vector<double> A(n * n), AP(n * (n + 1) / 2);
+    for (int64_t i = 0; i < n; ++i)
+        for (int64_t j = 0; j < n; ++j) A[i + j * n] = 0.5 * (M[i + j * n] + M[j + i * n]);
+    for (int64_t j = 0; j < n; ++j)
+        for (int64_t i = 0; i <= j; ++i) AP[i + j * (j + 1) / 2] = A[i + j * n];   // ColMajor upper packed
+    RandBLAS::DenseSkOp<double> S(RandBLAS::DenseDist(d, n), 4);
+    std::vector<double> B1(d * n), B2(d * n), B3(d * n);
+    RandBLAS::sketch_general(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, n, 1.0, S, A.data(), n, 0.0, B1.data(), d);
+    RandBLAS::sketch_symmetric(Layout::ColMajor, 1.0, S, A.data(), n, 0.0, B2.data(), d);
+    RandBLAS::ext::sketch_symmetric_triangle(blas::Side::Left, Layout::ColMajor, blas::Uplo::Upper, true, d, n, 1.0, S,
+                                             (int64_t)0, (int64_t)0, AP.data(), (int64_t)0, 0.0, B3.data(), d);
+    for (int64_t e = 0; e < d * n; ++e) {
+        CHECK(B2[e] == B1[e]);
+        CHECK(B3[e] == B1[e]);
+    }
+}
+
 int main() {
 #ifdef ONLY_SKSP   // diagnostics: the sketch_sparse checks alone
     try {
@@ -423,6 +447,7 @@ int main() {
     output_padding_untouched();
     sparse_operator_state();
     spmm_both_sides();
+    symmetric_one_triangle();
     if (g_fail) {
         std::printf("%d checks FAILED\n", g_fail);
         return 1;

@@ -85,3 +85,168 @@ def test_require_symmetric_device(cuda, layout):
         rb.require_symmetric(layout, dev(buf2, cuda), n, n, 0.0)
     rb.require_symmetric(layout, dev(buf2, cuda), n, n, 1e-2)   # within tolerance
     rb.require_symmetric(layout, dev(buf2, cuda), n, n, -1.0)   # tol < 0 skips the check
+
+
+# --------------------------------------------------------------------------------------------
+# One-triangle reads: sketch_symmetric reads only A's upper triangle once the
+# device check found A bitwise symmetric; rbh_sksy_tri reads one triangle of full or packed storage
+# and never touches the other. The operand tiles are the same as with full storage, so the
+# results are compared BITWISE with sketch_general on the full symmetric matrix (itself checked
+# against the oracle within E elsewhere); one case per config is also checked against the oracle.
+# --------------------------------------------------------------------------------------------
+def sym_full(n, seed):
+    M = np.random.default_rng(seed).standard_normal((n, n))
+    return (M + M.T) * 0.5   # fl(a + b) = fl(b + a): bitwise symmetric
+
+
+def store(M, layout, lda):
+    n = M.shape[0]
+    buf = np.zeros(lda * n)
+    for j in range(n):
+        if layout == "C":
+            buf[j * lda:j * lda + n] = M[:, j]
+        else:
+            buf[j * lda:j * lda + n] = M[j, :]
+    return buf
+
+
+def packed(M, layout, uplo):
+    """BLAS packed storage of one triangle of symmetric M (ColMajor 'U': A(i,j) at i + j(j+1)/2, i <= j;
+    'L': at i + (2n - j - 1) j / 2, i >= j; RowMajor 'U' / 'L' are ColMajor 'L' / 'U' of the transpose)."""
+    n = M.shape[0]
+    i, j = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
+    if layout == "R":   # row-major packing of (i, j) = column-major packing of (j, i), other triangle
+        i, j = j, i
+        uplo = "L" if uplo == "U" else "U"
+    if uplo == "U":
+        sel = i <= j
+        idx = i + j * (j + 1) // 2
+    else:
+        sel = i >= j
+        idx = i + (2 * n - j - 1) * j // 2
+    AP = np.zeros(n * (n + 1) // 2)
+    AP[idx[sel]] = M[sel] if layout == "C" else M.T[sel]
+    return AP
+
+
+def poison_other_triangle(buf, n, lda, layout, uplo):
+    """NaN in every stored slot of the triangle that is NOT uplo (the diagonal stays)."""
+    out = buf.copy()
+    for j in range(n):
+        for i in range(n):
+            other = (i > j) if uplo == "U" else (i < j)
+            if other:
+                out[(i + j * lda) if layout == "C" else (i * lda + j)] = np.nan
+    return out
+
+
+def full_sketch(cuda, side, layout, d, n, M, dtype=np.float64, major="L", key=5, alpha=0.75, beta=0.0, B0=None,
+                S_buff=None):
+    lda = n
+    A = dev(store(M, layout, lda).astype(dtype), cuda)
+    sr, sc = (d, n) if side == "L" else (n, d)
+    S = rb.DenseSkOp(rb.DenseDist(sr + 3, sc + 5, "G", major), rb.RNGState(key))
+    if S_buff is not None:
+        S.buff, S.buff_layout = S_buff, "C"
+    br, bc = (d, n) if side == "L" else (n, d)
+    ldb = br if layout == "C" else bc
+    B = dev(B0.copy() if B0 is not None else np.zeros(br * bc, dtype), cuda)
+    if side == "L":
+        rb.sketch_general_left(layout, "N", "N", d, n, n, dtype(alpha), S, A, lda, dtype(beta), B, ldb, ro_s=2, co_s=4)
+    else:
+        rb.sketch_general_right(layout, "N", "N", n, d, n, dtype(alpha), A, lda, S, dtype(beta), B, ldb, ro_s=2,
+                                co_s=4)
+    return host(B), S, ldb
+
+
+@pytest.mark.parametrize("side", ["L", "R"])
+@pytest.mark.parametrize("layout", ["C", "R"])
+@pytest.mark.parametrize("n", [700, 1040])
+def test_sketch_symmetric_reads_one_triangle_bitwise(cuda, side, layout, n):
+    d = 96
+    M = sym_full(n, 3)
+    ref, S, ldb = full_sketch(cuda, side, layout, d, n, M)
+    br, bc = (d, n) if side == "L" else (n, d)
+    B = torch.zeros(br * bc, dtype=torch.float64, device=cuda)
+    A = dev(store(M, layout, n), cuda)
+    if side == "L":
+        rb.sketch_symmetric_left(layout, d, n, 0.75, S, A, n, 0.0, B, ldb, ro_s=2, co_s=4)
+    else:
+        rb.sketch_symmetric_right(layout, n, d, 0.75, A, n, S, 0.0, B, ldb, ro_s=2, co_s=4)
+    got = host(B)
+    assert np.array_equal(got.view(np.uint64), ref.view(np.uint64)), f"{np.sum(got != ref)} differ"
+
+
+def test_sketch_symmetric_triangle_vs_oracle(cuda):
+    """The one-triangle product against the oracle within the reference's bound E."""
+    d, n = 64, 1030
+    M = sym_full(n, 4)
+    Mstore = store(M, "C", n)
+    B = torch.zeros(d * n, dtype=torch.float64, device=cuda)
+    S = rb.DenseSkOp(rb.DenseDist(d, n), rb.RNGState(0))
+    rb.sketch_symmetric_left("C", d, n, 1.0, S, dev(Mstore, cuda), n, 0.0, B, d)
+    Bexp = np.zeros(d * n)
+    O.lskge3("C", "N", "N", d, n, n, 1.0, d, n, "G", "L", 0, 0, 0, Mstore, n, 0.0, Bexp, d)
+    Sx, _ = O.fill_dense("C", d, n, "G", "L", d, n, 0, 0, key=0)
+    E = O.error_bound_left("C", "N", "N", d, n, n, 1.0, np.abs(Sx), d, Mstore, n, 0.0, np.zeros(d * n), d, np.float64)
+    assert np.all(np.abs(host(B) - Bexp) <= E)
+
+
+@pytest.mark.parametrize("side", ["L", "R"])
+@pytest.mark.parametrize("layout", ["C", "R"])
+@pytest.mark.parametrize("uplo", ["U", "L"])
+@pytest.mark.parametrize("fmt", ["F", "P"])
+def test_sksy_tri_full_and_packed(cuda, side, layout, uplo, fmt):
+    """rbh_sksy_tri: only triangle uplo is read (the other holds NaN), beta != 0, full or packed."""
+    d, n = 80, 600
+    M = sym_full(n, 6)
+    br, bc = (d, n) if side == "L" else (n, d)
+    B0 = np.random.default_rng(2).standard_normal(br * bc)
+    ref, S, ldb = full_sketch(cuda, side, layout, d, n, M, beta=-0.5, B0=B0)
+    if fmt == "F":
+        lda = n + 3
+        A = poison_other_triangle(store(M, layout, lda), n, lda, layout, uplo)
+    else:
+        lda, A = 0, packed(M, layout, uplo)
+    B = dev(B0, cuda)
+    rb.sketch_symmetric_tri(layout, side, uplo, fmt, d, n, 0.75, S, dev(A, cuda), lda, -0.5, B, ldb, ro_s=2, co_s=4)
+    got = host(B)
+    assert np.array_equal(got.view(np.uint64), ref.view(np.uint64)), f"{np.sum(got != ref)} differ"
+
+
+@pytest.mark.parametrize("case", ["f32", "short_axis", "explicit_S", "unaligned_n"])
+def test_sksy_tri_fallbacks(cuda, case):
+    """Where the fused one-triangle kernel does not apply (f32, a counter along the outer index,
+    an explicit S buffer, K % 16 != 0) the triangle is expanded and the plain kernels run: still
+    bitwise the full-storage product."""
+    d, n = 48, 500 if case != "unaligned_n" else 517
+    dtype = np.float32 if case == "f32" else np.float64
+    M = sym_full(n, 8).astype(dtype)
+    major = "S" if case == "short_axis" else "L"
+    S_buff = None
+    if case == "explicit_S":
+        Sx, _ = O.fill_dense("C", d + 3, n + 5, "G", "L", d + 3, n + 5, 0, 0, key=5)
+        S_buff = dev(Sx, cuda)
+    ref, S, ldb = full_sketch(cuda, "L", "C", d, n, M, dtype=dtype, major=major, S_buff=S_buff)
+    A = poison_other_triangle(store(M, "C", n), n, n, "C", "U").astype(dtype)
+    B = torch.zeros(d * n, dtype=torch.float64 if dtype == np.float64 else torch.float32, device=cuda)
+    rb.sketch_symmetric_tri("C", "L", "U", "F", d, n, dtype(0.75), S, dev(A, cuda), n, dtype(0.0), B, ldb, ro_s=2,
+                            co_s=4)
+    got = host(B)
+    ut = np.uint64 if dtype == np.float64 else np.uint32
+    assert np.array_equal(got.view(ut), ref.view(ut)), f"{np.sum(got != ref)} differ"
+
+
+def test_sketch_symmetric_not_bitwise_symmetric(cuda):
+    """A symmetric within tol > 0 but not bitwise: both triangles are read (the full-storage
+    product), as the reference computes it."""
+    d, n = 40, 520
+    M = sym_full(n, 9)
+    Mp = M.copy()
+    Mp[3, 400] += 1e-13
+    ref, S, ldb = full_sketch(cuda, "L", "C", d, n, Mp)
+    B = torch.zeros(d * n, dtype=torch.float64, device=cuda)
+    rb.sketch_symmetric_left("C", d, n, 0.75, S, dev(store(Mp, "C", n), cuda), n, 0.0, B, ldb, ro_s=2, co_s=4,
+                             sym_check_tol=1e-6)
+    got = host(B)
+    assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))
