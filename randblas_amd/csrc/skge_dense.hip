@@ -536,6 +536,15 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 #ifndef RBH_WIDE_WG
 #define RBH_WIDE_WG 1
 #endif
+#ifndef RBH_WIDE_IL
+#define RBH_WIDE_IL 0
+#endif
+#ifndef RBH_WIDE_IL_V
+#define RBH_WIDE_IL_V 4
+#endif
+#ifndef RBH_WIDE_DRAW_AT
+#define RBH_WIDE_DRAW_AT -1   // sub-step after whose MFMAs the drawing waves draw (-1: before the first)
+#endif
 // TRI != 0: the memory operand is a symmetric matrix of which only one triangle is read
 // (sketch_symmetric, sksy.hh:165-537, with A's other triangle never touched). In the operand's own
 // coordinates (o, k) the stored triangle is k <= o (TRI 1 full storage, 3 packed) or k >= o (2, 4);
@@ -722,7 +731,11 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) gv[e] = FAMILY == rb::UNIFORM ? (T)sm[e] * (T)gop.scale : (T)sm[e];
 #endif
+#if RBH_WIDE_IL
+        {   // branch-free (the draw shares its basic block with the MFMAs): edge masks as selects
+#else
         if (!gtile_full || kt * BK >= p.K) {   // uniform: edge tile or the prefetch past K
+#endif
             if (GK == GEN_OK) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) gv[e] = (glane_ok && kt * BK < p.K) ? gv[e] : (T)0;
@@ -771,6 +784,11 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
     const int gfa = (16 * FA * wg + r) * LDG + 4 * g;   // + 16 * a * LDG per fragment a
     const int mrow = (16 * FB * wmm + r) * BK;          // + 16 * c * BK per fragment c
     const int msw = (r >> 1) & 7;
+    // RBH_WIDE_IL: 0 = the drawing waves draw in a branch ahead of their MFMAs; 1 = two copies of
+    // the loop (drawing / not drawing waves), the draw in the MFMAs' basic block; 2 = as 1, with
+    // the drawing waves' MFMAs and draw VALU interleaved by sched_group_barrier
+    auto k_loop = [&](auto drawer_tag) {
+    constexpr bool DRAWER = decltype(drawer_tag)::value;
     for (int64_t kt = 0; kt < nk; ++kt) {
         const int cur = (int)(kt & 1);
         const T *Mc = lds + cur * MS;
@@ -783,7 +801,11 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
 #else
         dma(kn, cur ^ 1);
 #endif
-        if (wave < 4) draw(kt + 1);
+#if RBH_WIDE_IL
+        if (DRAWER) draw(kt + 1);
+#else
+        if (RBH_WIDE_DRAW_AT < 0 && wave < 4) draw(kt + 1);
+#endif
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
 #ifndef RBH_WIDE_DMA
@@ -804,17 +826,40 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
 #pragma unroll
                 for (int c = 0; c < FB; ++c)
                     acc[a][c] = GX ? Mfma<T>::mma(mf[c], gf[a], acc[a][c]) : Mfma<T>::mma(gf[a], mf[c], acc[a][c]);
+#if !RBH_WIDE_IL
+            if (s == RBH_WIDE_DRAW_AT && wave < 4) draw(kt + 1);   // after this sub-step's MFMAs are issued
+#endif
 #ifdef RBH_WIDE_SB
             __builtin_amdgcn_sched_barrier(0);
 #endif
         }
+#if RBH_WIDE_IL
+        if (DRAWER) gstore(cur ^ 1);
+#else
         if (wave < 4) gstore(cur ^ 1);
+#endif
 #ifndef RBH_WIDE_DMA
         if (TRI) rstore_tri(cur ^ 1, 1, cn);
         else rstore(cur ^ 1, 1);
 #endif
+#if RBH_WIDE_IL == 2
+        if (DRAWER) {
+#pragma unroll
+            for (int q = 0; q < 4 * FA * FB; ++q) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);              // one MFMA
+                __builtin_amdgcn_sched_group_barrier(0x002, RBH_WIDE_IL_V, 0);  // then draw VALU
+            }
+        }
+#endif
         __syncthreads();
     }
+    };
+#if RBH_WIDE_IL
+    if (wave < 4) k_loop(std::true_type{});
+    else k_loop(std::false_type{});
+#else
+    k_loop(std::false_type{});
+#endif
 
     T *C = (T *)p.C;
     const T alpha = (T)p.alpha, beta = (T)p.beta;
