@@ -90,8 +90,8 @@ __device__ __forceinline__ bool sp_locate_rc(int64_t r, int64_t c, const SparseA
     if (!(wr >= 0 && wr < p.win_r && wc >= 0 && wc < p.win_c)) return false;
     i = p.transposed ? wc : wr;
     const int64_t k = p.transposed ? wr : wc;
-    v = (k / SP_KC) * p.M + i;
-    kk = (uint32_t)(k % SP_KC);
+    v = (k >> p.kcs) * p.M + i;
+    kk = (uint32_t)(k & ((1 << p.kcs) - 1));
     return true;
 }
 
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(64) void fill_sparse_small_kernel(uint32_t c0, uint
             int64_t v, ii;
             uint32_t kk;
             if (sp_locate_rc(maj_is_row ? (int64_t)wl : i, maj_is_row ? i : (int64_t)wl, p, v, kk, ii))
-                atomicOr(&mask[v * 4 + kk / 32], 1u << (kk % 32));
+                atomicOr(&mask[(v << (p.kcs - 5)) + kk / 32], 1u << (kk % 32));
         }
         // ctr_work.incr() (sparse_skops.hh:91): 128-bit add of one
         ctr[0] += 1u;
@@ -891,43 +891,33 @@ __global__ __launch_bounds__(SU_NT) void saso_unit_kernel(const SparseApply p, c
 // ------------------------------------------------------------------------------------------
 // 5. Uniform-value apply with LDS-DMA staging (f64): sampled operators (values +-1) with
 //    |alpha| = 1, so P = Y exactly. The walk is section 4's, but nothing is loaded into VGPRs
-//    while it runs: the next chunk's panel and CSR records, and the row bounds of the chunk after,
-//    are copied global -> LDS with global_load_lds (no VGPR destination), issued before the walk
-//    and drained at the chunk's barrier, so the copies overlap the walk (section 4's loads must
-//    complete before GPR index mode is switched on).
+//    while it runs: the panels of the next NBUF - 1 chunks of KC contracted indices, and the row
+//    bounds of the chunk after next, are copied global -> LDS with global_load_lds (no VGPR
+//    destination), so the copies overlap the walk and up to (NBUF - 1) x 32 KiB (KC = 64) are in
+//    flight per CU.
+//    Per chunk ch: wait for panel ch and bounds ch -> barrier (every wave is done with chunk
+//    ch - 1, whose buffer takes panel ch + NBUF - 1) -> issue bounds ch + 2 and panel ch + NBUF - 1
+//    -> walk chunk ch.
 //    Panel layouts, unpadded; the walk address is lane_base ^ koff:
-//      * Y contiguous along k (YJ = false): [64 columns][SP_KC]; 16-B vector v of column c sits in
+//      * Y contiguous along k (YJ = false): [64 columns][KC]; 16-B vector v of column c sits in
 //        slot v ^ (c & 15), which spreads the 64 lanes' reads of one k over the banks;
 //        koff = k * sizeof(T).
-//      * Y contiguous along j (YJ = true): [SP_KC][64 columns]; koff = k * 64 * sizeof(T).
+//      * Y contiguous along j (YJ = true): [KC][64 columns]; koff = k * 64 * sizeof(T).
 //    Padding records add into a dummy accumulator register (v[96:97]), so no zero element.
-//    A wave's records of a chunk are one contiguous CSR range. By default they are read with
-//    scalar loads (s_load_dwordx8 x 6) straight into SGPRs, SD_SW = 48 per window, so an entry costs
-//    three VALU (address, sign, add) and three SALU ops, no readlane; the last one to three
-//    entries of a window are padded to a batch of four. Measured at C3: 0.731 -> 0.677 ms.
-//    With -DSD_NO_SMEM the workgroup's records are staged in LDS instead (up to SD_RCAP, mean at
-//    C3: 512; the rest read from HBM before their window) and taken with v_readlane.
+//    A wave's records of a chunk are one contiguous CSR range, read with scalar loads
+//    (s_load_dwordx8 x 6) straight into SGPRs, SD_SW = 48 per window, so an entry costs three VALU
+//    (address, sign, add) and three SALU ops and no readlane; the last one to three entries of a
+//    window are padded to a batch of four.
 // ------------------------------------------------------------------------------------------
-constexpr int SD_RCAP = 2048;
-#ifndef SD_SW_DEF
-#define SD_SW_DEF 48   // C3: 0.708 ms with 32-record windows, 0.692 ms with 48 (one window for most waves)
-#endif
-constexpr int SD_SW = SD_SW_DEF;   // records per scalar-load window (32 or 48)
-   // (default walk; -DSD_NO_SMEM: LDS records + readlane)
-// LDS reads of the walk stay in flight across the index-mode add (measured: no effect on the
-// results, 6 % faster than draining them); -DSD_DRAIN_LDS restores the drain
-#ifdef SD_DRAIN_LDS
-#define SD_DRAIN "s_waitcnt lgkmcnt(0)\n\t"
-#else
-#define SD_DRAIN ""
-#endif
+constexpr int SD_SW = 48;   // records per scalar-load window (C3: 0.708 ms with 32, 0.692 ms with 48)
 
-template <typename T> struct SdCfg {
+template <int KC, int NBUF> struct SdCfg {
+    typedef double T;
     static constexpr int VEC = 16 / (int)sizeof(T);
-    static constexpr int PANEL_B = SP_KC * SU_J * (int)sizeof(T);   // bytes per panel buffer
-    static constexpr int REC_OFF = 2 * PANEL_B;
-    static constexpr int BND_OFF = REC_OFF + 2 * SD_RCAP * 4;
-    static constexpr int MAIN_B = BND_OFF + 4 * 64 * 4;
+    static constexpr int PANEL_B = KC * SU_J * (int)sizeof(T);   // bytes per panel buffer
+    static constexpr int BND_OFF = NBUF * PANEL_B;               // row bounds: a ring of 4 chunks
+    static constexpr int FLAG_OFF = BND_OFF + 4 * 64 * 4;       // NBUF = 4: landed[4], walked[4]
+    static constexpr int MAIN_B = FLAG_OFF + 8 * 4;
     static constexpr int EPI_B = SuCfg<T>::EPI * (int)sizeof(T);
     static constexpr int BYTES = MAIN_B > EPI_B ? MAIN_B : EPI_B;
     static constexpr uint32_t PAD = 64u;   // padding record: the dummy's register index, koff 0, sign +
@@ -940,76 +930,22 @@ struct SdAcc {
     double dmy;
     __device__ __forceinline__ double get(int r) const { return r < 16 ? a[r] : b[r - 16]; }
     __device__ __forceinline__ void set(int r, double x) { if (r < 16) a[r] = x; else b[r - 16] = x; }
-    __device__ __forceinline__ void add_at(uint32_t rec, double y) {
-        uint32_t m;
-        asm("s_and_b32 %0, %1, 0x80000000" : "=s"(m) : "s"(rec) : "scc");
-        const double ys = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, y) ^ ((uint64_t)m << 32));
-        asm volatile(SD_DRAIN
-                     "s_set_gpr_idx_on %3, gpr_idx(SRC0,DST)\n\t"
-                     "v_add_f64 v[32:33], v[32:33], %4\n\t"
-                     "s_set_gpr_idx_off"
-                     : "+{v[32:63]}"(a), "+{v[64:95]}"(b), "+{v[96:97]}"(dmy)
-                     : "s"(rec), "v"(ys)
-                     : "m0", "scc");
-    }
 };
 
-#ifndef SD_NO_BATCH
-#define SD_BATCH 1
-#endif
-#ifndef SD_PRE
-#define SD_PRE ""   // diagnostics: an instruction string placed before the index-mode section
-#endif
-#ifdef SD_BATCH
-// four entries in one index-mode section: the row index moves with s_set_gpr_idx_idx, so the mode
-// is toggled once per four adds (the sign flips are done before the section)
-#ifdef SD_FMA
-// sign on the scalar side: fma(y, +-1.0, acc) rounds once, exactly as acc + (+-y), so the entry
-// costs one VALU op (the +-1.0 pair is built by SALU from the record's sign bit)
-__device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t *w, const double *y, uint32_t cm) {
-    uint64_t sg[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        uint32_t hi;
-        asm("s_and_b32 %0, %1, 0x80000000\n\t"
-            "s_or_b32 %0, %0, 0x3ff00000"
-            : "=&s"(hi) : "s"(w[q]) : "scc");
-        sg[q] = (uint64_t)hi << 32;
-    }
-    asm volatile("s_set_gpr_idx_on %3, gpr_idx(SRC2,DST)\n\t"
-                 "v_fma_f64 v[32:33], %7, %11, v[32:33]\n\t"
-                 "s_set_gpr_idx_idx %4\n\t"
-                 "v_fma_f64 v[32:33], %8, %12, v[32:33]\n\t"
-                 "s_set_gpr_idx_idx %5\n\t"
-                 "v_fma_f64 v[32:33], %9, %13, v[32:33]\n\t"
-                 "s_set_gpr_idx_idx %6\n\t"
-                 "v_fma_f64 v[32:33], %10, %14, v[32:33]\n\t"
-                 "s_set_gpr_idx_off"
-                 : "+{v[32:63]}"(acc.a), "+{v[64:95]}"(acc.b), "+{v[96:97]}"(acc.dmy)
-                 : "s"(w[0]), "s"(w[1]), "s"(w[2]), "s"(w[3]), "v"(y[0]), "v"(y[1]), "v"(y[2]), "v"(y[3]),
-                   "s"(sg[0]), "s"(sg[1]), "s"(sg[2]), "s"(sg[3])
-                 : "m0", "scc");
-}
-#else
-__device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t *w, const double *y, uint32_t cm) {
+// Four entries in one index-mode section: the row index moves with s_set_gpr_idx_idx, so the mode
+// is toggled once per four adds (the sign flips are done before the section). LDS reads of the
+// walk stay in flight across the section: like the compiler's own index-mode code (which keeps
+// VMEM loads in flight across s_set_gpr_idx_on), index mode changes only the VGPR operands of VALU
+// instructions.
+__device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t *w, const double *y) {
     double ys[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        uint32_t m;
-#ifdef SD_VSIGN
-        // sign on the vector side: hi ^ (record & 0x80000000) in one v_bitop3 (table 0x78 =
-        // S0 ^ (S1 & S2)), no SALU op
-        (void)m;   // cm: 0x80000000 in a VGPR, materialised once by the kernel
-        const uint64_t yb = __builtin_bit_cast(uint64_t, y[q]);
-        uint32_t hi = (uint32_t)(yb >> 32);
-        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x78" : "=v"(hi) : "v"(hi), "s"(w[q]), "v"(cm));
-        ys[q] = __builtin_bit_cast(double, ((uint64_t)hi << 32) | (yb & 0xffffffffull));
-#else
+        uint32_t m;   // sign mask made opaque, so the xor is not fused into a v_bitop3 reading the SGPR
         asm("s_and_b32 %0, %1, 0x80000000" : "=s"(m) : "s"(w[q]) : "scc");
         ys[q] = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, y[q]) ^ ((uint64_t)m << 32));
-#endif
     }
-    asm volatile(SD_PRE "s_set_gpr_idx_on %3, gpr_idx(SRC0,DST)\n\t"
+    asm volatile("s_set_gpr_idx_on %3, gpr_idx(SRC0,DST)\n\t"
                  "v_add_f64 v[32:33], v[32:33], %7\n\t"
                  "s_set_gpr_idx_idx %4\n\t"
                  "v_add_f64 v[32:33], v[32:33], %8\n\t"
@@ -1022,8 +958,6 @@ __device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t *w, const dou
                  : "s"(w[0]), "s"(w[1]), "s"(w[2]), "s"(w[3]), "v"(ys[0]), "v"(ys[1]), "v"(ys[2]), "v"(ys[3])
                  : "m0", "scc");
 }
-#endif
-#endif
 
 __device__ __forceinline__ uint32_t lds_addr(const void *ptr) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)ptr;
@@ -1049,17 +983,32 @@ __device__ __forceinline__ void dma4(const void *g, uint32_t m0) {
                  : "memory", "m0");
 }
 
-template <bool YJ>
-__global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, const int32_t *vrp,
+// s_waitcnt vmcnt(N) with N a compile-time count
+template <int N> __device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+#ifdef SD_PROF
+// Diagnostic build only (-DSD_PROF): per-phase cycle totals of the DMA apply, summed over waves.
+// 0 wait for copies, 1 barrier, 2 copy issue, 3 bounds, 4 record loads, 5 walk, 6 entries, 7 chunks
+__device__ unsigned long long rbh_sd_prof[8];
+#define SD_T(slot) do { const uint64_t now_ = clock64(); pf[slot] += now_ - pf_t; pf_t = now_; } while (0)
+#else
+#define SD_T(slot) do { } while (0)
+#endif
+
+template <bool YJ, int KC, int NBUF>
+__global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, const int32_t *seg,
                                                          const uint32_t *rec32, int64_t nchunks, int64_t nrb,
                                                          int vec_out) {
     typedef double T;
-    typedef SdCfg<T> G;
+    typedef SdCfg<KC, NBUF> G;
     constexpr int VEC = G::VEC;
+    static_assert(NBUF == 2 || NBUF == 4, "panel ring of 2 or 4 buffers");
     __shared__ __attribute__((aligned(16))) char smem[G::BYTES];
     const char *lbase = smem;
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
-    const uint32_t *recs = reinterpret_cast<const uint32_t *>(smem + G::REC_OFF);
     const int32_t *bnd = reinterpret_cast<const int32_t *>(smem + G::BND_OFF);
 
     const int tid = threadIdx.x;
@@ -1077,8 +1026,6 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     const T *Y = (const T *)p.Y;
     const T beta = (T)p.beta;
 
-    uint32_t sgnmask = 0x80000000u;   // sign-bit mask in a VGPR (SD_VSIGN)
-    asm volatile("" : "+v"(sgnmask));
     SdAcc acc;
     acc.dmy = (T)0;
     if (beta != (T)0) {
@@ -1092,24 +1039,30 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
         for (int r = 0; r < SU_R; ++r) acc.set(r, (T)0);
     }
 
-    // row bounds of chunk cc: bnd[(cc & 3) * 64 + l] = start of wave l's rows, l <= 16 (l = 16: end)
+    // record bounds of chunk cc: bnd[(cc & 3) * 64 + l] = start of wave l's records, l <= 16 (l = 16:
+    // end); seg[] has one entry per (chunk, group of SU_R rows), NG groups per chunk, and a closing
+    // entry; wave 0 copies them (one instruction)
+    const int64_t NG = (p.M + SU_R - 1) / SU_R;
+    const int64_t grp0 = rb0 / SU_R;
     auto dma_bounds = [&](int64_t cc) {
         if (wave == 0) {
             const int64_t l = lane < 16 ? lane : 16;
-            const int64_t r = rb0 + SU_R * l < p.M ? rb0 + SU_R * l : p.M;
-            dma4(vrp + cc * p.M + r, lds0 + G::BND_OFF + (uint32_t)((cc & 3) * 256));
+            const int64_t g = grp0 + l < NG ? grp0 + l : NG;
+            dma4(seg + cc * NG + g, lds0 + G::BND_OFF + (uint32_t)((cc & 3) * 256));
         }
     };
-    // panel of chunk cc -> buffer cc & 1; 1 KB per instruction, out-of-range sources clamped (the
-    // elements they bring are never read: no record points at k >= K, columns >= N are not stored)
+    // panel of chunk cc -> buffer cc % NBUF; 1 KB per instruction, NI per wave; out-of-range sources
+    // clamped (the elements they bring are never read: no record points at k >= K, columns >= N
+    // are not stored)
+    constexpr int NI = KC * SU_J * (int)sizeof(T) / 1024 / 16;
+    static_assert(NI >= 1, "whole instructions per wave");
     auto dma_panel = [&](int64_t cc) {
-        const uint32_t pb = lds0 + (uint32_t)((cc & 1) * G::PANEL_B);
-        const int64_t kc0 = cc * SP_KC;
+        const uint32_t pb = lds0 + (uint32_t)((cc % NBUF) * G::PANEL_B);
+        const int64_t kc0 = cc * KC;
         if (!YJ) {
-            constexpr int COLB = SP_KC * (int)sizeof(T);   // bytes per column
-            constexpr int CPI = 1024 / COLB;              // columns per instruction
-            constexpr int SPC = COLB / 16;                // 16-B slots per column
-            constexpr int NI = SU_J / CPI / 16;           // instructions per wave
+            constexpr int COLB = KC * (int)sizeof(T);   // bytes per column
+            constexpr int CPI = 1024 / COLB;            // columns per instruction
+            constexpr int SPC = COLB / 16;              // 16-B slots per column
 #pragma unroll
             for (int i = 0; i < NI; ++i) {
                 const int inst = wave * NI + i;
@@ -1120,10 +1073,9 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
                 dma16(Y + gj * p.ysj + gk, pb + (uint32_t)(inst * 1024));
             }
         } else {
-            constexpr int RB = SU_J * (int)sizeof(T);     // bytes per panel row
-            constexpr int RPI = 1024 / RB;                // rows per instruction
-            constexpr int VPR = RB / 16;                  // 16-B vectors per row
-            constexpr int NI = SP_KC / RPI / 16;          // instructions per wave
+            constexpr int RB = SU_J * (int)sizeof(T);   // bytes per panel row
+            constexpr int RPI = 1024 / RB;              // rows per instruction
+            constexpr int VPR = RB / 16;                // 16-B vectors per row
 #pragma unroll
             for (int i = 0; i < NI; ++i) {
                 const int inst = wave * NI + i;
@@ -1133,49 +1085,48 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
             }
         }
     };
-    // the workgroup's records of chunk cc (bounds already in LDS) -> recs[(cc & 1) * SD_RCAP ..]
-    auto dma_recs = [&](int64_t cc) {
-        const int32_t *bb = bnd + (cc & 3) * 64;
-        const int B0 = __builtin_amdgcn_readfirstlane(bb[0]), B1 = __builtin_amdgcn_readfirstlane(bb[16]);
-        const int n = B1 - B0 < SD_RCAP ? B1 - B0 : SD_RCAP;
-        for (int q = wave; q * 64 < n; q += 16) {
-            const int e = B0 + q * 64 + (int)lane;
-            dma4(rec32 + (e < B1 ? e : B0), lds0 + G::REC_OFF + (uint32_t)(((cc & 1) * SD_RCAP + q * 64) * 4));
-        }
-    };
-
-    dma_bounds(0);
-    if (nchunks > 1) dma_bounds(1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-#ifdef SD_NO_SMEM
-    dma_recs(0);
-#endif
-    dma_panel(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
 
     const uint32_t lanebase = YJ ? lane * (uint32_t)sizeof(T)
-                                 : lane * (uint32_t)(SP_KC * sizeof(T)) + 16u * (lane & 15u);
-    for (int64_t ch = 0; ch < nchunks; ++ch) {
-        if (ch + 1 < nchunks) {
-#ifdef SD_NO_SMEM
-            dma_recs(ch + 1);
+                                 : lane * (uint32_t)(KC * sizeof(T)) + 16u * (lane & 15u);
+#ifdef SD_PROF
+    uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t pf_t = clock64();
 #endif
-            if (!(p.ablate & 2)) dma_panel(ch + 1);   // diagnostics: ablate 2 skips the panel copies
-        }
-        if (ch + 2 < nchunks) dma_bounds(ch + 2);
+    // A wave's records of chunk ch: rec32[gofs, gofs + ne), ne a multiple of 4 (every (chunk, wave)
+    // segment is padded with padding records); bounds in slot ch & 3
+    auto chunk_range = [&](int64_t ch, int &gofs, int &ne) {
         const int32_t *bb = bnd + (ch & 3) * 64;
-        const int B0 = __builtin_amdgcn_readfirstlane(bb[0]);
-        const int eb = __builtin_amdgcn_readfirstlane(bb[wave]) - B0;
-        int ne = __builtin_amdgcn_readfirstlane(bb[wave + 1]) - B0 - eb;
-        // a sampled operator has no duplicate (row, k): at most SU_R * SP_KC entries per wave
-        ne = ne < 0 ? 0 : (ne > SU_R * SP_KC ? SU_R * SP_KC : ne);
-        const uint32_t L = lanebase + (uint32_t)((ch & 1) * G::PANEL_B);
-        const uint32_t *rbuf = recs + (ch & 1) * SD_RCAP;
-#ifndef SD_NO_SMEM
-        // records come straight from HBM/L2 into SGPRs (scalar loads), one window at a time: no
-        // readlane per entry. Entries past the window's end are padding records.
+        gofs = __builtin_amdgcn_readfirstlane(bb[wave]);
+        ne = __builtin_amdgcn_readfirstlane(bb[wave + 1]) - gofs;
+#ifdef SD_PROF
+        SD_T(3);
+        pf[6] += ne > 0 ? ne : 0;
+        pf[7] += 1;
+#endif
+        // a sampled operator has no duplicate (row, k): at most SU_R * KC entries per wave
+        ne = ne < 0 ? 0 : (ne > SU_R * KC ? SU_R * KC : ne);
+        if (p.ablate & 1) ne = 0;   // ablate 1: no walk
+    };
+    // Records come straight from HBM/L2 into SGPRs (scalar loads), SD_SW at a time. The loads and
+    // their wait are one asm statement, so no SGPR destination is visible to the compiler before the
+    // data has landed; PRE is spliced in between (the lock-step ring puts its vmcnt wait and barrier
+    // there, which hides the load latency of a chunk's first window).
+    typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+    u32x8 r0, r1, r2, r3, r4, r5;
+#define SD_LOAD_WINDOW(GW, PRE)                                                                      \
+    asm volatile("s_load_dwordx8 %0, %6, 0x0\n\t"                                                    \
+                 "s_load_dwordx8 %1, %6, 0x20\n\t"                                                   \
+                 "s_load_dwordx8 %2, %6, 0x40\n\t"                                                   \
+                 "s_load_dwordx8 %3, %6, 0x60\n\t"                                                   \
+                 "s_load_dwordx8 %4, %6, 0x80\n\t"                                                   \
+                 "s_load_dwordx8 %5, %6, 0xa0\n\t" PRE                                               \
+                 "s_waitcnt lgkmcnt(0)"                                                              \
+                 : "=&s"(r0), "=&s"(r1), "=&s"(r2), "=&s"(r3), "=&s"(r4), "=&s"(r5)                  \
+                 : "s"(GW)                                                                           \
+                 : "memory")
+    // walk of chunk ch (panel in buffer ch % NBUF); the first window is in r0 .. r5
+    auto walk_chunk = [&](int64_t ch, int gofs, int ne) {
+        const uint32_t L = lanebase + (uint32_t)((ch % NBUF) * G::PANEL_B);
         auto walk = [&](const uint32_t (&wr)[SD_SW], int nw) {
             auto issue = [&](int x0, T (&y)[SU_D], uint32_t (&w)[SU_D]) {
 #pragma unroll
@@ -1184,36 +1135,18 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
                     y[q] = *reinterpret_cast<const T *>(lbase + (L ^ ((w[q] >> 8) & 0xfffffu)));
                 }
             };
-            constexpr int WIN = SD_SW;
-#else
-        auto walk = [&](uint32_t rc, int nw) {
-            auto issue = [&](int x0, T (&y)[SU_D], uint32_t (&w)[SU_D]) {
-#pragma unroll
-                for (int q = 0; q < SU_D; ++q) {
-                    w[q] = (uint32_t)__builtin_amdgcn_readlane((int)rc, x0 + q);
-                    y[q] = *reinterpret_cast<const T *>(lbase + (L ^ ((w[q] >> 8) & 0xfffffu)));
-                }
-            };
-            constexpr int WIN = SU_WIN;
-#endif
             auto update = [&](const T (&y)[SU_D], const uint32_t (&w)[SU_D]) {
-#ifdef SD_BATCH
                 static_assert(SU_D % 4 == 0, "batched update takes four entries at a time");
 #pragma unroll
-                for (int g = 0; g < SU_D; g += 4) sd_add4(acc, w + g, y + g, sgnmask);
-#else
-#pragma unroll
-                for (int q = 0; q < SU_D; ++q) acc.add_at(w[q], y[q]);
-#endif
+                for (int g = 0; g < SU_D; g += 4) sd_add4(acc, w + g, y + g);
             };
             T ya[SU_D], yb[SU_D];
             uint32_t wa[SU_D], wb[SU_D];
             issue(0, ya, wa);
             const int nsteps = (nw + SU_D - 1) / SU_D;
-#ifndef SD_LOOP
-            // straight-line walk (a window has at most SU_WIN entries): constant lane indices for
-            // the readlanes, and no loop-carried wait state for the compiler to merge
-            constexpr int MAXS = (WIN + SU_D - 1) / SU_D;
+            // straight-line walk (a window has at most SD_SW entries): no loop-carried wait state;
+            // an issue past the last step reads a stale record's LDS slot, which no add uses
+            constexpr int MAXS = (SD_SW + SU_D - 1) / SU_D;
 #pragma unroll
             for (int s2 = 0; s2 < MAXS; s2 += 2) {
                 if (s2 >= nsteps) break;
@@ -1223,96 +1156,115 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
                 issue((s2 + 2) * SU_D, ya, wa);
                 update(yb, wb);
             }
-#else
-#pragma unroll 1
-            for (int s2 = 0; s2 < nsteps; s2 += 2) {
-                issue((s2 + 1) * SU_D, yb, wb);
-                update(ya, wa);
-                if (s2 + 1 >= nsteps) break;
-                issue((s2 + 2) * SU_D, ya, wa);
-                update(yb, wb);
-            }
-#endif
         };
-        if (p.ablate & 1) ne = 0;   // diagnostics: ablate 1 skips the walk
-#ifndef SD_NO_SMEM
         for (int done = 0; done < ne; done += SD_SW) {
-            const int nw = ne - done < SD_SW ? ne - done : SD_SW;
-            const uint32_t *gw = rec32 + B0 + eb + done;   // rec32 is padded by SD_SW records
-            typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
-            u32x8 r0, r1, r2, r3;
+            if (done > 0) SD_LOAD_WINDOW(rec32 + gofs + done, "");
+            SD_T(4);
             uint32_t wr[SD_SW];
-            if constexpr (SD_SW == 48) {
-                // all six loads and their wait in one statement: no SGPR destination is visible to
-                // the compiler before the data has landed
-                u32x8 r4, r5;
-                asm volatile("s_load_dwordx8 %0, %6, 0x0\n\t"
-                             "s_load_dwordx8 %1, %6, 0x20\n\t"
-                             "s_load_dwordx8 %2, %6, 0x40\n\t"
-                             "s_load_dwordx8 %3, %6, 0x60\n\t"
-                             "s_load_dwordx8 %4, %6, 0x80\n\t"
-                             "s_load_dwordx8 %5, %6, 0xa0\n\t"
-                             "s_waitcnt lgkmcnt(0)"
-                             : "=&s"(r0), "=&s"(r1), "=&s"(r2), "=&s"(r3), "=&s"(r4), "=&s"(r5)
-                             : "s"(gw)
-                             : "memory");
 #pragma unroll
-                for (int q = 0; q < 8; ++q) { wr[32 + q] = r4[q]; wr[40 + q] = r5[q]; }
-            } else {
-                asm volatile("s_load_dwordx8 %0, %4, 0x0\n\t"
-                             "s_load_dwordx8 %1, %4, 0x20\n\t"
-                             "s_load_dwordx8 %2, %4, 0x40\n\t"
-                             "s_load_dwordx8 %3, %4, 0x60\n\t"
-                             "s_waitcnt lgkmcnt(0)"
-                             : "=&s"(r0), "=&s"(r1), "=&s"(r2), "=&s"(r3)
-                             : "s"(gw)
-                             : "memory");
+            for (int q = 0; q < 8; ++q) {
+                wr[q] = r0[q]; wr[8 + q] = r1[q]; wr[16 + q] = r2[q];
+                wr[24 + q] = r3[q]; wr[32 + q] = r4[q]; wr[40 + q] = r5[q];
             }
-#pragma unroll
-            for (int q = 0; q < 8; ++q) { wr[q] = r0[q]; wr[8 + q] = r1[q]; wr[16 + q] = r2[q]; wr[24 + q] = r3[q]; }
-            // whole steps of four straight from the window, no per-entry selects (an issue past
-            // the last step reads a stale record's LDS slot, which no add uses)
-            const int nfull = nw & ~3;
-            if (nfull > 0) walk(wr, nfull);
-            if (nw & 3) {   // the last one to three entries, padded to a step of four
-                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-                u32x4 rt;
-                asm volatile("s_load_dwordx4 %0, %1, 0x0\n\t"
-                             "s_waitcnt lgkmcnt(0)"
-                             : "=&s"(rt)
-                             : "s"(gw + nfull)
-                             : "memory");
-                uint32_t w4[4];
-                T y4[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    w4[q] = q < (nw & 3) ? rt[q] : G::PAD;
-                    y4[q] = *reinterpret_cast<const T *>(lbase + (L ^ ((w4[q] >> 8) & 0xfffffu)));
-                }
-                sd_add4(acc, w4, y4, sgnmask);
-            }
+            walk(wr, ne - done < SD_SW ? ne - done : SD_SW);
+            SD_T(5);
         }
-#else
-        for (int done = 0; done < ne; done += SU_WIN) {
-            const int nw = ne - done < SU_WIN ? ne - done : SU_WIN;
-            const int rel = eb + done + (int)lane;
-            uint32_t rc;
-            if (eb + done + nw <= SD_RCAP) {
-                const uint32_t x = rbuf[rel < SD_RCAP ? rel : 0];
-                rc = (int)lane < nw ? x : G::PAD;
-            } else {   // past the staged records (rare): from HBM, complete before the walk
-                const uint32_t x = rec32[B0 + ((int)lane < nw ? rel : eb)];
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                rc = (int)lane < nw ? x : G::PAD;
-            }
-            walk(rc, nw);
-        }
-#endif
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+
+    if constexpr (NBUF == 2) {
+        // lock-step ring: panel ch + 1 goes into the buffer chunk ch - 1 used, after a barrier
+        dma_bounds(0);
+        if (nchunks > 1) dma_bounds(1);
+        if (nchunks > 0) dma_panel(0);
+        wait_vm<0>();
         __syncthreads();
+        for (int64_t ch = 0; ch < nchunks; ++ch) {
+            int gofs, ne;
+            chunk_range(ch, gofs, ne);   // bounds ch: landed before the previous barrier
+            // first record window, then (while it loads) wait for this wave's copies of panel ch
+            // and bounds ch + 1 and meet the other waves: every copy for chunk ch is in LDS, and
+            // chunk ch - 1 is walked
+            SD_LOAD_WINDOW(rec32 + gofs, "s_waitcnt vmcnt(0)\n\ts_barrier\n\t");
+            SD_T(1);
+            if (ch + 2 < nchunks) dma_bounds(ch + 2);
+            if (ch + 1 < nchunks && !(p.ablate & 2)) dma_panel(ch + 1);   // ablate 2: no copies
+            SD_T(2);
+            walk_chunk(ch, gofs, ne);
+        }
+    } else {
+        // Flag ring, no barrier per chunk. Chunk c's copies (bounds by wave 0, a share of the panel
+        // by every wave) go to slot c % 4; they are issued three chunks ahead, after the issuing
+        // wave has walked chunk c - 3 and every wave has walked chunk c - 4, the slot's previous
+        // tenant. After walking chunk c - 2 a wave waits for its own copies of chunk c (s_waitcnt
+        // vmcnt, only chunk c + 1's may still be in flight) and adds one to landed[c & 3]; chunk c
+        // is walked once all 16 have. Counters only grow: chunk x is complete in a counter of
+        // slot x & 3 at 16 (x / 4 + 1). So waves drift up to two chunks apart, and copy-issue
+        // stalls, record-load latency and the binomial spread of entries per wave overlap instead
+        // of adding up at a barrier.
+        uint32_t *landed = reinterpret_cast<uint32_t *>(smem + G::FLAG_OFF);
+        uint32_t *walked = landed + 4;
+        if (tid < 8) landed[tid] = 0;
+        __syncthreads();
+        // bounded: a protocol error gives wrong sums (which the parity tests see), never a hang
+        auto spin_until = [&](const uint32_t *f, uint32_t target) {
+            for (int it = 0; it < (1 << 22); ++it) {
+                const uint32_t v = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                if ((int32_t)(v - target) >= 0) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            asm volatile("" ::: "memory");
+        };
+        auto signal = [&](uint32_t *f) {
+            asm volatile("" ::: "memory");
+            if (lane == 0) __hip_atomic_fetch_add(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        };
+        constexpr uint32_t NW = SU_NT / 64;
+        auto done_at = [&](int64_t x) { return NW * (uint32_t)((x >> 2) + 1); };
+        auto issue = [&](int64_t cc) {
+            dma_bounds(cc);
+            if (!(p.ablate & 2)) dma_panel(cc);
+        };
+        // this wave's copies of every chunk issued before the last `later` groups have landed
+        auto wait_groups = [&](int later) {
+            if (p.ablate & 2) wait_vm<0>();
+            else if (later >= 1) { if (wave == 0) wait_vm<NI + 1>(); else wait_vm<NI>(); }
+            else wait_vm<0>();
+        };
+        for (int c = 0; c < 3; ++c)
+            if (c < nchunks) issue(c);
+        wait_groups(nchunks > 2 ? 1 : 0);
+        signal(landed + 0);
+        if (nchunks > 1) signal(landed + 1);
+        for (int64_t ch = 0; ch < nchunks; ++ch) {
+            spin_until(landed + (ch & 3), done_at(ch));
+            SD_T(1);
+            int gofs, ne;
+            chunk_range(ch, gofs, ne);
+            SD_LOAD_WINDOW(rec32 + gofs, "");
+            walk_chunk(ch, gofs, ne);
+            signal(walked + (ch & 3));
+            if (ch + 3 < nchunks) {
+                if (ch >= 1) spin_until(walked + ((ch - 1) & 3), done_at(ch - 1));
+                issue(ch + 3);
+            }
+            SD_T(2);
+            if (ch + 2 < nchunks) {
+                wait_groups(ch + 3 < nchunks ? 1 : 0);
+                signal(landed + ((ch + 2) & 3));
+            }
+            SD_T(0);
+        }
     }
+#ifdef SD_PROF
+    if (lane == 0)
+        for (int q = 0; q < 8; ++q) atomicAdd(&rbh_sd_prof[q], (unsigned long long)pf[q]);
+#endif
+    wait_vm<0>();
+    __syncthreads();   // the epilogue reuses the panel memory
     su_epilogue<T>(acc, reinterpret_cast<T *>(smem), p, row0, j0, wave, lane, vec_out);
 }
+#undef SD_LOAD_WINDOW
 
 // ------------------------------------------------------------------------------------------
 // 6. CSR / CSC pointer arrays -> per-entry major indices (sketch_sparse's data matrix as COO):
@@ -1332,7 +1284,8 @@ hipError_t launch_expand_ptr(int64_t n_major, const int64_t *ptr, int64_t *out, 
 
 // ------------------------------------------------------------------------------------------
 // 7. CSR build without a sort, for operators whose (row, k) entries are distinct (every sampled
-//    SASO / LASO): bit (k % SP_KC) of mask[v] marks an entry of virtual row v; the entry's CSR
+//    SASO / LASO): bit (k % KC) of mask[v] marks an entry of virtual row v (KC = 2^p.kcs, the
+//    DMA apply's chunk depth, KC / 32 mask words per virtual row); the entry's CSR
 //    position is the row's start plus the number of marked bits below it, i.e. its rank in
 //    ascending k -- the order the sort produces.
 // ------------------------------------------------------------------------------------------
@@ -1345,9 +1298,11 @@ __device__ __forceinline__ bool sp_locate(int64_t e, const int64_t *rows, const 
 struct MaskPopcount {
     const uint32_t *mask;
     int64_t NV;
+    int mw;   // mask words per virtual row: 2 or 4
     __device__ __host__ int32_t operator()(int64_t v) const {
-        return v < NV ? __popc(mask[4 * v]) + __popc(mask[4 * v + 1]) + __popc(mask[4 * v + 2]) + __popc(mask[4 * v + 3])
-                      : 0;
+        if (v >= NV) return 0;
+        const uint32_t *m = mask + mw * v;
+        return mw == 2 ? __popc(m[0]) + __popc(m[1]) : __popc(m[0]) + __popc(m[1]) + __popc(m[2]) + __popc(m[3]);
     }
 };
 
@@ -1356,48 +1311,97 @@ __global__ void mark_kernel(int64_t nnz, const int64_t *rows, const int64_t *col
     const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     int64_t v, i;
     uint32_t kk;
-    if (e < nnz && sp_locate(e, rows, cols, p, v, kk, i)) atomicOr(&mask[v * 4 + kk / 32], 1u << (kk % 32));
+    if (e < nnz && sp_locate(e, rows, cols, p, v, kk, i)) atomicOr(&mask[(v << (p.kcs - 5)) + kk / 32], 1u << (kk % 32));
 }
 
+// records of segment g = (chunk, group of SU_R rows: one wave's rows), padded to a multiple of 4
+// (g == NGT: the scan's closing zero)
+struct SegPadCount {
+    const int32_t *vrp;
+    int64_t M, NG, NGT;
+    __device__ __host__ int32_t operator()(int64_t g) const {
+        if (g >= NGT) return 0;
+        const int64_t ch = g / NG, r0 = (g % NG) * SU_R;
+        const int64_t r1 = r0 + SU_R < M ? r0 + SU_R : M;
+        return (vrp[ch * M + r1] - vrp[ch * M + r0] + 3) & ~3;
+    }
+};
+
+// An entry's record goes to its segment's start + the entries of the segment's earlier rows + its
+// rank in its row (ascending k).
 template <typename T>
 __global__ void place_kernel(int64_t nnz, const int64_t *rows, const int64_t *cols, const T *vals, const SparseApply p,
-                             const uint32_t *mask, const int32_t *vrp, uint32_t *rec, uint32_t kmul) {
+                             const uint32_t *mask, const int32_t *vrp, const int32_t *seg, uint32_t *rec,
+                             uint32_t kmul) {
     const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     int64_t v, i;
     uint32_t kk;
     if (e >= nnz || !sp_locate(e, rows, cols, p, v, kk, i)) return;
-    const uint32_t *mw = mask + 4 * v;
+    const uint32_t *mw = mask + (v << (p.kcs - 5));
     uint32_t rank = __popc(mw[kk / 32] & ((1u << (kk % 32)) - 1u));
     for (uint32_t w = 0; w < kk / 32; ++w) rank += __popc(mw[w]);
+    const int64_t ch = (v - i) / p.M, grp = i / SU_R;
+    const int64_t NG = (p.M + SU_R - 1) / SU_R;
+    const int64_t pos = seg[ch * NG + grp] + (vrp[v] - vrp[ch * p.M + grp * SU_R]) + rank;
     const uint32_t row = (uint32_t)(i % 32);
     const T x = (T)p.alpha * vals[e];
-    rec[vrp[v] + rank] = (sizeof(T) == 8 ? 2u * row : row) | ((kk * kmul) << 8) | (signbit(x) ? 0x80000000u : 0u);
+    rec[pos] = (sizeof(T) == 8 ? 2u * row : row) | ((kk * kmul) << 8) | (signbit(x) ? 0x80000000u : 0u);
 }
 
 // The LDS-DMA apply (section 5) on a sort-free CSR. With gen, the operator is sampled here into
 // the workspace and its entries marked in the same pass (fill_sparse_small_kernel<.., true>).
-static hipError_t run_sparse_dma(const SparseApply &p, const SparseGen *gen, const int64_t *rows, const int64_t *cols,
+// Chunk depth and panel ring (RBH_SASO_KC = 64 | 128, RBH_SASO_NBUF = 2 | 4 for measurements).
+struct DmaShape { int kc, nbuf; };
+static DmaShape dma_shape() {
+    static const DmaShape sh = [] {
+        DmaShape d{128, 2};
+        const char *k = getenv("RBH_SASO_KC");
+        const char *b = getenv("RBH_SASO_NBUF");
+        if (k && atoi(k) == 64) d.kc = 64;
+        if (b && atoi(b) == 4) d.nbuf = 4;
+        if (d.kc == 128) d.nbuf = 2;   // 4 x 64 KiB panels do not fit in LDS
+        return d;
+    }();
+    return sh;
+}
+
+static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, const int64_t *rows, const int64_t *cols,
                                  const double *vals, int64_t nnz, bool y_k, hipStream_t s) {
-    const int64_t nchunks = p.K > 0 ? (p.K + SP_KC - 1) / SP_KC : 0;
+    const DmaShape sh = dma_shape();
+    SparseApply p = p0;
+    p.kcs = sh.kc == 128 ? 7 : 6;
+    const int mw = sh.kc / 32;
+    const int64_t nchunks = p.K > 0 ? (p.K + sh.kc - 1) / sh.kc : 0;
     const int64_t NV = nchunks * p.M;
     const size_t n = (size_t)(nnz > 0 ? nnz : 1);
-    const MaskPopcount pc0{nullptr, NV};
+    const int64_t NG = (p.M + SU_R - 1) / SU_R;
+    const int64_t NGT = nchunks * NG;
+    const size_t nrec = n + 3 * (size_t)NGT + SD_SW;   // + segment padding + scalar-window overrun
+    if (nrec >= (size_t)0x7fffffff) return hipErrorNotSupported;   // int32 record offsets
+    const MaskPopcount pc0{nullptr, NV, mw};
     auto cnt_it0 = rocprim::make_transform_iterator(rocprim::counting_iterator<int64_t>(0), pc0);
-    size_t scan_bytes = 0;
+    size_t scan_bytes = 0, scan2_bytes = 0;
     hipError_t err = rocprim::exclusive_scan(nullptr, scan_bytes, cnt_it0, (int32_t *)nullptr, 0, (size_t)(NV + 1),
                                              rocprim::plus<int32_t>(), s);
     if (err != hipSuccess) return err;
+    const SegPadCount sp0{nullptr, p.M, NG, NGT};
+    auto seg_it0 = rocprim::make_transform_iterator(rocprim::counting_iterator<int64_t>(0), sp0);
+    err = rocprim::exclusive_scan(nullptr, scan2_bytes, seg_it0, (int32_t *)nullptr, 0, (size_t)(NGT + 1),
+                                  rocprim::plus<int32_t>(), s);
+    if (err != hipSuccess) return err;
+    if (scan2_bytes > scan_bytes) scan_bytes = scan2_bytes;
     const size_t gen_bytes = gen ? n * (2 * sizeof(int64_t) + sizeof(double)) + 64 : 0;
-    const size_t bytes = (size_t)NV * 16 + (size_t)(NV + 1) * sizeof(int32_t) + (n + SD_SW) * sizeof(uint32_t) + scan_bytes +
-                         gen_bytes + 256;
+    const size_t bytes = (size_t)NV * 4 * mw + (size_t)(NV + 1) * sizeof(int32_t) + (size_t)(NGT + 1) * sizeof(int32_t) +
+                         nrec * sizeof(uint32_t) + scan_bytes + gen_bytes + 256;
     char *ws = nullptr;
     err = ws_alloc((void **)&ws, bytes, s);
     if (err != hipSuccess) return err;
     size_t off = 0;
     auto carve = [&](size_t b) { void *q = ws + off; off += (b + 15) & ~(size_t)15; return q; };
-    uint32_t *mask = (uint32_t *)carve((size_t)NV * 16);
+    uint32_t *mask = (uint32_t *)carve((size_t)NV * 4 * mw);
     int32_t *vrp = (int32_t *)carve((size_t)(NV + 1) * sizeof(int32_t));
-    uint32_t *rec = (uint32_t *)carve((n + SD_SW) * sizeof(uint32_t));   // + scalar-window overrun
+    int32_t *seg = (int32_t *)carve((size_t)(NGT + 1) * sizeof(int32_t));
+    uint32_t *rec = (uint32_t *)carve(nrec * sizeof(uint32_t));
     void *tmp = carve(scan_bytes);
     if (gen) {
         int64_t *gr = (int64_t *)carve(n * sizeof(int64_t));
@@ -1406,7 +1410,8 @@ static hipError_t run_sparse_dma(const SparseApply &p, const SparseGen *gen, con
         rows = gr; cols = gc; vals = gv;
     }
     const uint32_t kmul = y_k ? (uint32_t)sizeof(double) : (uint32_t)(SU_J * sizeof(double));
-    err = hipMemsetAsync(mask, 0, (size_t)NV * 16, s);
+    err = hipMemsetAsync(mask, 0, (size_t)NV * 4 * mw, s);
+    if (err == hipSuccess) err = hipMemsetD32Async(rec, (int)SdCfg<64, 2>::PAD, nrec, s);   // padding records
     if (err == hipSuccess && gen) {
         err = launch_fill_sparse_t<double>(*gen, (int64_t *)rows, (int64_t *)cols, (double *)vals, s, &p, mask);
     } else if (err == hipSuccess && nnz > 0) {
@@ -1414,13 +1419,18 @@ static hipError_t run_sparse_dma(const SparseApply &p, const SparseGen *gen, con
         err = hipGetLastError();
     }
     if (err == hipSuccess) {
-        const MaskPopcount pc{mask, NV};
+        const MaskPopcount pc{mask, NV, mw};
         auto cnt_it = rocprim::make_transform_iterator(rocprim::counting_iterator<int64_t>(0), pc);
         err = rocprim::exclusive_scan(tmp, scan_bytes, cnt_it, vrp, 0, (size_t)(NV + 1), rocprim::plus<int32_t>(), s);
     }
+    if (err == hipSuccess) {
+        const SegPadCount sp{vrp, p.M, NG, NGT};
+        auto seg_it = rocprim::make_transform_iterator(rocprim::counting_iterator<int64_t>(0), sp);
+        err = rocprim::exclusive_scan(tmp, scan_bytes, seg_it, seg, 0, (size_t)(NGT + 1), rocprim::plus<int32_t>(), s);
+    }
     if (err == hipSuccess && nnz > 0) {
         hipLaunchKernelGGL(place_kernel<double>, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, rows, cols,
-                           vals, p, mask, vrp, rec, kmul);
+                           vals, p, mask, vrp, seg, rec, kmul);
         err = hipGetLastError();
     }
     if (err == hipSuccess) {
@@ -1428,14 +1438,30 @@ static hipError_t run_sparse_dma(const SparseApply &p, const SparseGen *gen, con
         const int64_t nrb_u = (p.M + SU_ROWS - 1) / SU_ROWS;
         const dim3 grid_u((unsigned)(((p.N + SU_J - 1) / SU_J) * nrb_u));
         const int vec_out = p.crs == 1 && (p.ccs % 2) == 0 && (((uintptr_t)p.C) % 16) == 0;
-        if (y_k) hipLaunchKernelGGL((saso_dma_kernel<false>), grid_u, dim3(SU_NT), 0, s, p, vrp, rec, nchunks, nrb_u, vec_out);
-        else hipLaunchKernelGGL((saso_dma_kernel<true>), grid_u, dim3(SU_NT), 0, s, p, vrp, rec, nchunks, nrb_u, vec_out);
+#define RBH_SD(YJ, KC, NB) \
+    hipLaunchKernelGGL((saso_dma_kernel<YJ, KC, NB>), grid_u, dim3(SU_NT), 0, s, p, seg, rec, nchunks, nrb_u, vec_out)
+        if (sh.kc == 128) { if (y_k) RBH_SD(false, 128, 2); else RBH_SD(true, 128, 2); }
+        else if (sh.nbuf == 2) { if (y_k) RBH_SD(false, 64, 2); else RBH_SD(true, 64, 2); }
+        else { if (y_k) RBH_SD(false, 64, 4); else RBH_SD(true, 64, 4); }
+#undef RBH_SD
         err = hipGetLastError();
         timing_end(s);
     }
     hipError_t e2 = ws_free(ws, s);
     return err != hipSuccess ? err : e2;
 }
+
+#ifdef SD_PROF
+extern "C" int rbh_diag_saso_prof(unsigned long long *out, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rbh_sd_prof), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(rbh_sd_prof), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 
 // The DMA kernel's conditions: f64, values +-1 (sampled operator: distinct entries), |alpha| = 1
 // (the panel is Y itself), Y contiguous along k or j in 16-B vectors.
@@ -1454,8 +1480,10 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
     if (nnz >= (int64_t)0x7fffffff) return hipErrorInvalidValue;
     {   // LDS-DMA kernel (section 5) on the sort-free CSR (section 7)
         bool y_k;
-        if (sizeof(T) == 8 && dma_eligible(p, y_k))
-            return run_sparse_dma(p, nullptr, rows, cols, (const double *)vals, nnz, y_k, s);
+        if (sizeof(T) == 8 && dma_eligible(p, y_k)) {
+            const hipError_t e = run_sparse_dma(p, nullptr, rows, cols, (const double *)vals, nnz, y_k, s);
+            if (e != hipErrorNotSupported) return e;   // NotSupported: too many records, nothing done
+        }
     }
     hipError_t err;
     const int64_t nchunks = p.K > 0 ? (p.K + SP_KC - 1) / SP_KC : 0;
@@ -1551,8 +1579,10 @@ static hipError_t run_sparse_sampled_t(const SparseApply &p0, const SparseGen &g
     const int64_t dim_major = g.major_axis == 'S' ? short_ax : long_ax;
     bool y_k = false;
     if (sizeof(T) == 8 && p.M > 0 && p.N > 0 && nnz > 0 && g.vec_nnz <= SF_NZ && dim_major < ((int64_t)1 << 31) &&
-        dma_eligible(p, y_k))
-        return run_sparse_dma(p, &g, nullptr, nullptr, nullptr, nnz, y_k, s);
+        dma_eligible(p, y_k)) {
+        const hipError_t e = run_sparse_dma(p, &g, nullptr, nullptr, nullptr, nnz, y_k, s);
+        if (e != hipErrorNotSupported) return e;   // NotSupported: too many records, nothing done
+    }
     const size_t n = (size_t)(nnz > 0 ? nnz : 1);
     char *ws = nullptr;
     hipError_t err = ws_alloc((void **)&ws, n * (2 * sizeof(int64_t) + sizeof(T)), s);

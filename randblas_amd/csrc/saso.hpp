@@ -27,6 +27,7 @@ struct SparseApply {
     int64_t crs, ccs;
     int ablate;   // diagnostics only (env RBH_SASO_ABLATE): 1 = skip the entry walk, 2 = skip the panel loads
     int unit_vals;   // every value is +1 or -1 (operator sampled by fill_sparse in this call)
+    int kcs;         // LDS-DMA apply (saso.hip section 5): log2 of its chunk depth; set by the apply itself
 };
 
 hipError_t launch_fill_sparse_f64(const SparseGen &g, int64_t *rows, int64_t *cols, double *vals, hipStream_t s);
