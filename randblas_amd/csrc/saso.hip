@@ -891,33 +891,35 @@ __global__ __launch_bounds__(SU_NT) void saso_unit_kernel(const SparseApply p, c
 // ------------------------------------------------------------------------------------------
 // 5. Uniform-value apply with LDS-DMA staging (f64): sampled operators (values +-1) with
 //    |alpha| = 1, so P = Y exactly. The walk is section 4's, but nothing is loaded into VGPRs
-//    while it runs: the panels of the next NBUF - 1 chunks of KC contracted indices, and the row
-//    bounds of the chunk after next, are copied global -> LDS with global_load_lds (no VGPR
-//    destination), so the copies overlap the walk and up to (NBUF - 1) x 32 KiB (KC = 64) are in
-//    flight per CU.
-//    Per chunk ch: wait for panel ch and bounds ch -> barrier (every wave is done with chunk
-//    ch - 1, whose buffer takes panel ch + NBUF - 1) -> issue bounds ch + 2 and panel ch + NBUF - 1
-//    -> walk chunk ch.
+//    while it runs: the panel of the next chunk of KC contracted indices (64 KiB) and the record
+//    bounds of the chunk after it are copied global -> LDS with global_load_lds (no VGPR
+//    destination), so the copies overlap the walk.
+//    Per chunk ch: load the wave's first record window and, while it loads, wait for this wave's
+//    copies of panel ch and bounds ch + 1 and meet the other waves at a barrier (every copy for
+//    chunk ch is in LDS; chunk ch - 1 is walked, its buffer free) -> read bounds ch + 1 -> issue
+//    bounds ch + 2 and panel ch + 1 -> walk chunk ch.
 //    Panel layouts, unpadded; the walk address is lane_base ^ koff:
 //      * Y contiguous along k (YJ = false): [64 columns][KC]; 16-B vector v of column c sits in
 //        slot v ^ (c & 15), which spreads the 64 lanes' reads of one k over the banks;
 //        koff = k * sizeof(T).
 //      * Y contiguous along j (YJ = true): [KC][64 columns]; koff = k * 64 * sizeof(T).
-//    Padding records add into a dummy accumulator register (v[96:97]), so no zero element.
-//    A wave's records of a chunk are one contiguous CSR range, read with scalar loads
-//    (s_load_dwordx8 x 6) straight into SGPRs, SD_SW = 48 per window, so an entry costs three VALU
-//    (address, sign, add) and three SALU ops and no readlane; the last one to three entries of a
-//    window are padded to a batch of four.
+//    Records: one contiguous segment per (chunk, wave's 32 rows), padded to a multiple of four with
+//    padding records, which add into a dummy accumulator register (v[96:97]); read with scalar
+//    loads (s_load_dwordx8 x 6) straight into SGPRs, SD_SW = 48 per window, so an entry costs
+//    three VALU (address, sign, add) and three SALU ops and no readlane.
+//    Measured on C3 and kept out: 64-deep chunks with 2, 3 or 4 panels,
+//    a flag ring instead of the barrier, a rotating or dedicated copy wave, copies interleaved
+//    with the walk, an L2 prefetch of the panel after next.
 // ------------------------------------------------------------------------------------------
-constexpr int SD_SW = 48;   // records per scalar-load window (C3: 0.708 ms with 32, 0.692 ms with 48)
+constexpr int SD_KC = 128;   // contracted indices per chunk
+constexpr int SD_SW = 48;    // records per scalar-load window (C3: 0.708 ms with 32, 0.692 ms with 48)
 
-template <int KC, int NBUF> struct SdCfg {
+struct SdCfg {
     typedef double T;
     static constexpr int VEC = 16 / (int)sizeof(T);
-    static constexpr int PANEL_B = KC * SU_J * (int)sizeof(T);   // bytes per panel buffer
-    static constexpr int BND_OFF = NBUF * PANEL_B;               // row bounds: a ring of 4 chunks
-    static constexpr int FLAG_OFF = BND_OFF + 4 * 64 * 4;       // NBUF = 4: landed[4], walked[4]
-    static constexpr int MAIN_B = FLAG_OFF + 8 * 4;
+    static constexpr int PANEL_B = SD_KC * SU_J * (int)sizeof(T);   // bytes per panel buffer
+    static constexpr int BND_OFF = 2 * PANEL_B;                     // record bounds: a ring of 4 chunks
+    static constexpr int MAIN_B = BND_OFF + 4 * 64 * 4;
     static constexpr int EPI_B = SuCfg<T>::EPI * (int)sizeof(T);
     static constexpr int BYTES = MAIN_B > EPI_B ? MAIN_B : EPI_B;
     static constexpr uint32_t PAD = 64u;   // padding record: the dummy's register index, koff 0, sign +
@@ -934,9 +936,9 @@ struct SdAcc {
 
 // Four entries in one index-mode section: the row index moves with s_set_gpr_idx_idx, so the mode
 // is toggled once per four adds (the sign flips are done before the section). LDS reads of the
-// walk stay in flight across the section: like the compiler's own index-mode code (which keeps
-// VMEM loads in flight across s_set_gpr_idx_on), index mode changes only the VGPR operands of VALU
-// instructions.
+// walk stay in flight across the section. Index mode relocates the VGPR operands of VALU
+// instructions; LLVM's own index-mode code (SIInsertWaitcnts has no drain rule for
+// s_set_gpr_idx_on) keeps memory returns in flight across it the same way.
 __device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t *w, const double *y) {
     double ys[4];
 #pragma unroll
@@ -990,22 +992,23 @@ template <int N> __device__ __forceinline__ void wait_vm() {
 }
 
 #ifdef SD_PROF
-// Diagnostic build only (-DSD_PROF): per-phase cycle totals of the DMA apply, summed over waves.
-// 0 wait for copies, 1 barrier, 2 copy issue, 3 bounds, 4 record loads, 5 walk, 6 entries, 7 chunks
+// Diagnostic build only (-DSD_PROF, tools/build_saso_var.sh + tools/saso_prof.py): per-phase cycle
+// totals of the DMA apply, summed over waves: 1 record load + barrier, 2 copy issue, 3 bounds,
+// 4 later record windows, 5 walk; 6 entries, 7 wave-chunks.
 __device__ unsigned long long rbh_sd_prof[8];
 #define SD_T(slot) do { const uint64_t now_ = clock64(); pf[slot] += now_ - pf_t; pf_t = now_; } while (0)
 #else
 #define SD_T(slot) do { } while (0)
 #endif
 
-template <bool YJ, int KC, int NBUF>
+template <bool YJ>
 __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, const int32_t *seg,
                                                          const uint32_t *rec32, int64_t nchunks, int64_t nrb,
                                                          int vec_out) {
     typedef double T;
-    typedef SdCfg<KC, NBUF> G;
+    typedef SdCfg G;
+    constexpr int KC = SD_KC;
     constexpr int VEC = G::VEC;
-    static_assert(NBUF == 2 || NBUF == 4, "panel ring of 2 or 4 buffers");
     __shared__ __attribute__((aligned(16))) char smem[G::BYTES];
     const char *lbase = smem;
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
@@ -1051,34 +1054,30 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
             dma4(seg + cc * NG + g, lds0 + G::BND_OFF + (uint32_t)((cc & 3) * 256));
         }
     };
-    // panel of chunk cc -> buffer cc % NBUF; 1 KB per instruction, NI per wave; out-of-range sources
+    // panel of chunk cc -> buffer cc & 1; 1 KB per instruction, NI per wave; out-of-range sources
     // clamped (the elements they bring are never read: no record points at k >= K, columns >= N
     // are not stored)
     constexpr int NI = KC * SU_J * (int)sizeof(T) / 1024 / 16;
     static_assert(NI >= 1, "whole instructions per wave");
     auto dma_panel = [&](int64_t cc) {
-        const uint32_t pb = lds0 + (uint32_t)((cc % NBUF) * G::PANEL_B);
+        const uint32_t pb = lds0 + (uint32_t)((cc & 1) * G::PANEL_B);
         const int64_t kc0 = cc * KC;
-        if (!YJ) {
-            constexpr int COLB = KC * (int)sizeof(T);   // bytes per column
-            constexpr int CPI = 1024 / COLB;            // columns per instruction
-            constexpr int SPC = COLB / 16;              // 16-B slots per column
 #pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                const int inst = wave * NI + i;
+        for (int i = 0; i < NI; ++i) {
+            const int inst = wave * NI + i;
+            if (!YJ) {
+                constexpr int COLB = KC * (int)sizeof(T);   // bytes per column
+                constexpr int CPI = 1024 / COLB;            // columns per instruction
+                constexpr int SPC = COLB / 16;              // 16-B slots per column
                 const int col = inst * CPI + (int)lane / SPC;
                 const int v = ((int)lane % SPC) ^ (col & 15);
                 const int64_t gj = j0 + col < p.N ? j0 + col : p.N - 1;
                 const int64_t gk = kc0 + VEC * v < p.K ? kc0 + VEC * v : 0;
                 dma16(Y + gj * p.ysj + gk, pb + (uint32_t)(inst * 1024));
-            }
-        } else {
-            constexpr int RB = SU_J * (int)sizeof(T);   // bytes per panel row
-            constexpr int RPI = 1024 / RB;              // rows per instruction
-            constexpr int VPR = RB / 16;                // 16-B vectors per row
-#pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                const int inst = wave * NI + i;
+            } else {
+                constexpr int RB = SU_J * (int)sizeof(T);   // bytes per panel row
+                constexpr int RPI = 1024 / RB;              // rows per instruction
+                constexpr int VPR = RB / 16;                // 16-B vectors per row
                 const int64_t gk = kc0 + inst * RPI + (int)lane / VPR < p.K ? kc0 + inst * RPI + (int)lane / VPR : 0;
                 const int64_t gj = j0 + VEC * ((int)lane % VPR) < p.N ? j0 + VEC * ((int)lane % VPR) : 0;
                 dma16(Y + gk * p.ysk + gj, pb + (uint32_t)(inst * 1024));
@@ -1092,8 +1091,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t pf_t = clock64();
 #endif
-    // A wave's records of chunk ch: rec32[gofs, gofs + ne), ne a multiple of 4 (every (chunk, wave)
-    // segment is padded with padding records); bounds in slot ch & 3
+    // A wave's records of chunk ch: rec32[gofs, gofs + ne), ne a multiple of 4; bounds in slot ch & 3
     auto chunk_range = [&](int64_t ch, int &gofs, int &ne) {
         const int32_t *bb = bnd + (ch & 3) * 64;
         gofs = __builtin_amdgcn_readfirstlane(bb[wave]);
@@ -1109,24 +1107,21 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     };
     // Records come straight from HBM/L2 into SGPRs (scalar loads), SD_SW at a time. The loads and
     // their wait are one asm statement, so no SGPR destination is visible to the compiler before the
-    // data has landed; PRE is spliced in between (the lock-step ring puts its vmcnt wait and barrier
-    // there, which hides the load latency of a chunk's first window).
+    // data has landed (nor is a scalar load in flight while the compiler counts its own LDS reads
+    // with lgkmcnt); the first window of a chunk puts the copy wait and the barrier in between,
+    // which hides its load latency.
     typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
     u32x8 r0, r1, r2, r3, r4, r5;
-#define SD_LOAD_WINDOW(GW, PRE)                                                                      \
-    asm volatile("s_load_dwordx8 %0, %6, 0x0\n\t"                                                    \
-                 "s_load_dwordx8 %1, %6, 0x20\n\t"                                                   \
-                 "s_load_dwordx8 %2, %6, 0x40\n\t"                                                   \
-                 "s_load_dwordx8 %3, %6, 0x60\n\t"                                                   \
-                 "s_load_dwordx8 %4, %6, 0x80\n\t"                                                   \
-                 "s_load_dwordx8 %5, %6, 0xa0\n\t" PRE                                               \
-                 "s_waitcnt lgkmcnt(0)"                                                              \
-                 : "=&s"(r0), "=&s"(r1), "=&s"(r2), "=&s"(r3), "=&s"(r4), "=&s"(r5)                  \
-                 : "s"(GW)                                                                           \
-                 : "memory")
-    // walk of chunk ch (panel in buffer ch % NBUF); the first window is in r0 .. r5
+#define SD_LOADS                                                                                     \
+    "s_load_dwordx8 %0, %6, 0x0\n\t"                                                                  \
+    "s_load_dwordx8 %1, %6, 0x20\n\t"                                                                 \
+    "s_load_dwordx8 %2, %6, 0x40\n\t"                                                                 \
+    "s_load_dwordx8 %3, %6, 0x60\n\t"                                                                 \
+    "s_load_dwordx8 %4, %6, 0x80\n\t"                                                                 \
+    "s_load_dwordx8 %5, %6, 0xa0\n\t"
+    // walk of chunk ch (panel in buffer ch & 1); the first window is in r0 .. r5
     auto walk_chunk = [&](int64_t ch, int gofs, int ne) {
-        const uint32_t L = lanebase + (uint32_t)((ch % NBUF) * G::PANEL_B);
+        const uint32_t L = lanebase + (uint32_t)((ch & 1) * G::PANEL_B);
         auto walk = [&](const uint32_t (&wr)[SD_SW], int nw) {
             auto issue = [&](int x0, T (&y)[SU_D], uint32_t (&w)[SU_D]) {
 #pragma unroll
@@ -1158,7 +1153,11 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
             }
         };
         for (int done = 0; done < ne; done += SD_SW) {
-            if (done > 0) SD_LOAD_WINDOW(rec32 + gofs + done, "");
+            if (done > 0)
+                asm volatile(SD_LOADS "s_waitcnt lgkmcnt(0)"
+                             : "=&s"(r0), "=&s"(r1), "=&s"(r2), "=&s"(r3), "=&s"(r4), "=&s"(r5)
+                             : "s"(rec32 + gofs + done)
+                             : "memory");
             SD_T(4);
             uint32_t wr[SD_SW];
 #pragma unroll
@@ -1171,91 +1170,27 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
         }
     };
 
-    if constexpr (NBUF == 2) {
-        // lock-step ring: panel ch + 1 goes into the buffer chunk ch - 1 used, after a barrier
-        dma_bounds(0);
-        if (nchunks > 1) dma_bounds(1);
-        if (nchunks > 0) dma_panel(0);
-        wait_vm<0>();
-        __syncthreads();
-        for (int64_t ch = 0; ch < nchunks; ++ch) {
-            int gofs, ne;
-            chunk_range(ch, gofs, ne);   // bounds ch: landed before the previous barrier
-            // first record window, then (while it loads) wait for this wave's copies of panel ch
-            // and bounds ch + 1 and meet the other waves: every copy for chunk ch is in LDS, and
-            // chunk ch - 1 is walked
-            SD_LOAD_WINDOW(rec32 + gofs, "s_waitcnt vmcnt(0)\n\ts_barrier\n\t");
-            SD_T(1);
-            if (ch + 2 < nchunks) dma_bounds(ch + 2);
-            if (ch + 1 < nchunks && !(p.ablate & 2)) dma_panel(ch + 1);   // ablate 2: no copies
-            SD_T(2);
-            walk_chunk(ch, gofs, ne);
-        }
-    } else {
-        // Flag ring, no barrier per chunk. Chunk c's copies (bounds by wave 0, a share of the panel
-        // by every wave) go to slot c % 4; they are issued three chunks ahead, after the issuing
-        // wave has walked chunk c - 3 and every wave has walked chunk c - 4, the slot's previous
-        // tenant. After walking chunk c - 2 a wave waits for its own copies of chunk c (s_waitcnt
-        // vmcnt, only chunk c + 1's may still be in flight) and adds one to landed[c & 3]; chunk c
-        // is walked once all 16 have. Counters only grow: chunk x is complete in a counter of
-        // slot x & 3 at 16 (x / 4 + 1). So waves drift up to two chunks apart, and copy-issue
-        // stalls, record-load latency and the binomial spread of entries per wave overlap instead
-        // of adding up at a barrier.
-        uint32_t *landed = reinterpret_cast<uint32_t *>(smem + G::FLAG_OFF);
-        uint32_t *walked = landed + 4;
-        if (tid < 8) landed[tid] = 0;
-        __syncthreads();
-        // bounded: a protocol error gives wrong sums (which the parity tests see), never a hang
-        auto spin_until = [&](const uint32_t *f, uint32_t target) {
-            for (int it = 0; it < (1 << 22); ++it) {
-                const uint32_t v = __builtin_amdgcn_readfirstlane(
-                    __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-                if ((int32_t)(v - target) >= 0) break;
-                __builtin_amdgcn_s_sleep(1);
-            }
-            asm volatile("" ::: "memory");
-        };
-        auto signal = [&](uint32_t *f) {
-            asm volatile("" ::: "memory");
-            if (lane == 0) __hip_atomic_fetch_add(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        };
-        constexpr uint32_t NW = SU_NT / 64;
-        auto done_at = [&](int64_t x) { return NW * (uint32_t)((x >> 2) + 1); };
-        auto issue = [&](int64_t cc) {
-            dma_bounds(cc);
-            if (!(p.ablate & 2)) dma_panel(cc);
-        };
-        // this wave's copies of every chunk issued before the last `later` groups have landed
-        auto wait_groups = [&](int later) {
-            if (p.ablate & 2) wait_vm<0>();
-            else if (later >= 1) { if (wave == 0) wait_vm<NI + 1>(); else wait_vm<NI>(); }
-            else wait_vm<0>();
-        };
-        for (int c = 0; c < 3; ++c)
-            if (c < nchunks) issue(c);
-        wait_groups(nchunks > 2 ? 1 : 0);
-        signal(landed + 0);
-        if (nchunks > 1) signal(landed + 1);
-        for (int64_t ch = 0; ch < nchunks; ++ch) {
-            spin_until(landed + (ch & 3), done_at(ch));
-            SD_T(1);
-            int gofs, ne;
-            chunk_range(ch, gofs, ne);
-            SD_LOAD_WINDOW(rec32 + gofs, "");
-            walk_chunk(ch, gofs, ne);
-            signal(walked + (ch & 3));
-            if (ch + 3 < nchunks) {
-                if (ch >= 1) spin_until(walked + ((ch - 1) & 3), done_at(ch - 1));
-                issue(ch + 3);
-            }
-            SD_T(2);
-            if (ch + 2 < nchunks) {
-                wait_groups(ch + 3 < nchunks ? 1 : 0);
-                signal(landed + ((ch + 2) & 3));
-            }
-            SD_T(0);
-        }
+    dma_bounds(0);
+    if (nchunks > 1) dma_bounds(1);
+    if (nchunks > 0) dma_panel(0);
+    wait_vm<0>();
+    __syncthreads();
+    int gofs = 0, ne = 0;
+    if (nchunks > 0) chunk_range(0, gofs, ne);
+    for (int64_t ch = 0; ch < nchunks; ++ch) {
+        asm volatile(SD_LOADS "s_waitcnt vmcnt(0)\n\ts_barrier\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&s"(r0), "=&s"(r1), "=&s"(r2), "=&s"(r3), "=&s"(r4), "=&s"(r5)
+                     : "s"(rec32 + gofs)
+                     : "memory");
+        SD_T(1);
+        const int gofs_c = gofs, ne_c = ne;
+        if (ch + 1 < nchunks) chunk_range(ch + 1, gofs, ne);   // bounds ch + 1: visible since this barrier
+        if (ch + 2 < nchunks) dma_bounds(ch + 2);
+        if (ch + 1 < nchunks && !(p.ablate & 2)) dma_panel(ch + 1);   // ablate 2: no copies
+        SD_T(2);
+        walk_chunk(ch, gofs_c, ne_c);
     }
+#undef SD_LOADS
 #ifdef SD_PROF
     if (lane == 0)
         for (int q = 0; q < 8; ++q) atomicAdd(&rbh_sd_prof[q], (unsigned long long)pf[q]);
@@ -1264,7 +1199,6 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     __syncthreads();   // the epilogue reuses the panel memory
     su_epilogue<T>(acc, reinterpret_cast<T *>(smem), p, row0, j0, wave, lane, vec_out);
 }
-#undef SD_LOAD_WINDOW
 
 // ------------------------------------------------------------------------------------------
 // 6. CSR / CSC pointer arrays -> per-entry major indices (sketch_sparse's data matrix as COO):
@@ -1318,11 +1252,11 @@ __global__ void mark_kernel(int64_t nnz, const int64_t *rows, const int64_t *col
 // (g == NGT: the scan's closing zero)
 struct SegPadCount {
     const int32_t *vrp;
-    int64_t M, NG, NGT;
+    int64_t M, NG, NGT, R;   // R rows per segment
     __device__ __host__ int32_t operator()(int64_t g) const {
         if (g >= NGT) return 0;
-        const int64_t ch = g / NG, r0 = (g % NG) * SU_R;
-        const int64_t r1 = r0 + SU_R < M ? r0 + SU_R : M;
+        const int64_t ch = g / NG, r0 = (g % NG) * R;
+        const int64_t r1 = r0 + R < M ? r0 + R : M;
         return (vrp[ch * M + r1] - vrp[ch * M + r0] + 3) & ~3;
     }
 };
@@ -1332,7 +1266,7 @@ struct SegPadCount {
 template <typename T>
 __global__ void place_kernel(int64_t nnz, const int64_t *rows, const int64_t *cols, const T *vals, const SparseApply p,
                              const uint32_t *mask, const int32_t *vrp, const int32_t *seg, uint32_t *rec,
-                             uint32_t kmul) {
+                             uint32_t kmul, int R) {
     const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     int64_t v, i;
     uint32_t kk;
@@ -1340,43 +1274,30 @@ __global__ void place_kernel(int64_t nnz, const int64_t *rows, const int64_t *co
     const uint32_t *mw = mask + (v << (p.kcs - 5));
     uint32_t rank = __popc(mw[kk / 32] & ((1u << (kk % 32)) - 1u));
     for (uint32_t w = 0; w < kk / 32; ++w) rank += __popc(mw[w]);
-    const int64_t ch = (v - i) / p.M, grp = i / SU_R;
-    const int64_t NG = (p.M + SU_R - 1) / SU_R;
-    const int64_t pos = seg[ch * NG + grp] + (vrp[v] - vrp[ch * p.M + grp * SU_R]) + rank;
-    const uint32_t row = (uint32_t)(i % 32);
+    const int64_t ch = (v - i) / p.M, grp = i / R;
+    const int64_t NG = (p.M + R - 1) / R;
+    const int64_t pos = seg[ch * NG + grp] + (vrp[v] - vrp[ch * p.M + grp * R]) + rank;
+    const uint32_t row = (uint32_t)(i % R);
     const T x = (T)p.alpha * vals[e];
     rec[pos] = (sizeof(T) == 8 ? 2u * row : row) | ((kk * kmul) << 8) | (signbit(x) ? 0x80000000u : 0u);
 }
 
 // The LDS-DMA apply (section 5) on a sort-free CSR. With gen, the operator is sampled here into
 // the workspace and its entries marked in the same pass (fill_sparse_small_kernel<.., true>).
-// Chunk depth and panel ring (RBH_SASO_KC = 64 | 128, RBH_SASO_NBUF = 2 | 4 for measurements).
-struct DmaShape { int kc, nbuf; };
-static DmaShape dma_shape() {
-    static const DmaShape sh = [] {
-        DmaShape d{128, 2};
-        const char *k = getenv("RBH_SASO_KC");
-        const char *b = getenv("RBH_SASO_NBUF");
-        if (k && atoi(k) == 64) d.kc = 64;
-        if (b && atoi(b) == 4) d.nbuf = 4;
-        if (d.kc == 128) d.nbuf = 2;   // 4 x 64 KiB panels do not fit in LDS
-        return d;
-    }();
-    return sh;
-}
-
+// hipErrorNotSupported (nothing done): too many records for int32 offsets.
 static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, const int64_t *rows, const int64_t *cols,
                                  const double *vals, int64_t nnz, bool y_k, hipStream_t s) {
-    const DmaShape sh = dma_shape();
+    static_assert(SD_KC == 128, "kcs and mask words below");
     SparseApply p = p0;
-    p.kcs = sh.kc == 128 ? 7 : 6;
-    const int mw = sh.kc / 32;
-    const int64_t nchunks = p.K > 0 ? (p.K + sh.kc - 1) / sh.kc : 0;
+    p.kcs = 7;                           // log2(SD_KC)
+    const int mw = SD_KC / 32;           // mask words per virtual row
+    const int64_t nchunks = p.K > 0 ? (p.K + SD_KC - 1) / SD_KC : 0;
     const int64_t NV = nchunks * p.M;
     const size_t n = (size_t)(nnz > 0 ? nnz : 1);
-    const int64_t NG = (p.M + SU_R - 1) / SU_R;
+    const int64_t R = SU_R;              // rows per wave: records are segmented by them
+    const int64_t NG = (p.M + R - 1) / R;
     const int64_t NGT = nchunks * NG;
-    const size_t nrec = n + 3 * (size_t)NGT + SD_SW;   // + segment padding + scalar-window overrun
+    const size_t nrec = n + 3 * (size_t)NGT + 256;   // + segment padding + window / copy overrun (<= 255)
     if (nrec >= (size_t)0x7fffffff) return hipErrorNotSupported;   // int32 record offsets
     const MaskPopcount pc0{nullptr, NV, mw};
     auto cnt_it0 = rocprim::make_transform_iterator(rocprim::counting_iterator<int64_t>(0), pc0);
@@ -1384,7 +1305,7 @@ static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, co
     hipError_t err = rocprim::exclusive_scan(nullptr, scan_bytes, cnt_it0, (int32_t *)nullptr, 0, (size_t)(NV + 1),
                                              rocprim::plus<int32_t>(), s);
     if (err != hipSuccess) return err;
-    const SegPadCount sp0{nullptr, p.M, NG, NGT};
+    const SegPadCount sp0{nullptr, p.M, NG, NGT, R};
     auto seg_it0 = rocprim::make_transform_iterator(rocprim::counting_iterator<int64_t>(0), sp0);
     err = rocprim::exclusive_scan(nullptr, scan2_bytes, seg_it0, (int32_t *)nullptr, 0, (size_t)(NGT + 1),
                                   rocprim::plus<int32_t>(), s);
@@ -1411,7 +1332,7 @@ static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, co
     }
     const uint32_t kmul = y_k ? (uint32_t)sizeof(double) : (uint32_t)(SU_J * sizeof(double));
     err = hipMemsetAsync(mask, 0, (size_t)NV * 4 * mw, s);
-    if (err == hipSuccess) err = hipMemsetD32Async(rec, (int)SdCfg<64, 2>::PAD, nrec, s);   // padding records
+    if (err == hipSuccess) err = hipMemsetD32Async(rec, (int)SdCfg::PAD, nrec, s);   // padding records
     if (err == hipSuccess && gen) {
         err = launch_fill_sparse_t<double>(*gen, (int64_t *)rows, (int64_t *)cols, (double *)vals, s, &p, mask);
     } else if (err == hipSuccess && nnz > 0) {
@@ -1424,13 +1345,13 @@ static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, co
         err = rocprim::exclusive_scan(tmp, scan_bytes, cnt_it, vrp, 0, (size_t)(NV + 1), rocprim::plus<int32_t>(), s);
     }
     if (err == hipSuccess) {
-        const SegPadCount sp{vrp, p.M, NG, NGT};
+        const SegPadCount sp{vrp, p.M, NG, NGT, R};
         auto seg_it = rocprim::make_transform_iterator(rocprim::counting_iterator<int64_t>(0), sp);
         err = rocprim::exclusive_scan(tmp, scan_bytes, seg_it, seg, 0, (size_t)(NGT + 1), rocprim::plus<int32_t>(), s);
     }
     if (err == hipSuccess && nnz > 0) {
         hipLaunchKernelGGL(place_kernel<double>, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, rows, cols,
-                           vals, p, mask, vrp, seg, rec, kmul);
+                           vals, p, mask, vrp, seg, rec, kmul, (int)R);
         err = hipGetLastError();
     }
     if (err == hipSuccess) {
@@ -1438,12 +1359,8 @@ static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, co
         const int64_t nrb_u = (p.M + SU_ROWS - 1) / SU_ROWS;
         const dim3 grid_u((unsigned)(((p.N + SU_J - 1) / SU_J) * nrb_u));
         const int vec_out = p.crs == 1 && (p.ccs % 2) == 0 && (((uintptr_t)p.C) % 16) == 0;
-#define RBH_SD(YJ, KC, NB) \
-    hipLaunchKernelGGL((saso_dma_kernel<YJ, KC, NB>), grid_u, dim3(SU_NT), 0, s, p, seg, rec, nchunks, nrb_u, vec_out)
-        if (sh.kc == 128) { if (y_k) RBH_SD(false, 128, 2); else RBH_SD(true, 128, 2); }
-        else if (sh.nbuf == 2) { if (y_k) RBH_SD(false, 64, 2); else RBH_SD(true, 64, 2); }
-        else { if (y_k) RBH_SD(false, 64, 4); else RBH_SD(true, 64, 4); }
-#undef RBH_SD
+        if (y_k) hipLaunchKernelGGL((saso_dma_kernel<false>), grid_u, dim3(SU_NT), 0, s, p, seg, rec, nchunks, nrb_u, vec_out);
+        else hipLaunchKernelGGL((saso_dma_kernel<true>), grid_u, dim3(SU_NT), 0, s, p, seg, rec, nchunks, nrb_u, vec_out);
         err = hipGetLastError();
         timing_end(s);
     }

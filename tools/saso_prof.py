@@ -24,7 +24,7 @@ for it in range(4):
     assert fn(buf, 1) == 0
     if it == 0:
         continue
-    names = ["wait copies", "barrier", "copy issue", "bounds", "record loads", "walk"]
+    names = ["(unused)", "record load + barrier", "copy issue", "bounds", "later windows", "walk"]
     tot = sum(buf[q] for q in range(6))
     wc = buf[7]
     print(f"iter {it}: wave-chunks {wc}, entries/wave-chunk {buf[6] / max(wc, 1):.2f}, cycles/wave-chunk {tot / max(wc, 1):.0f}")
