@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2 GPU call 18: SASO after the variant cleanup: sparse parity (all sparse suites), C3 bench,
+# SASO check on one GPU box: sparse parity (all sparse suites), C3 bench,
 # phase timing.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
