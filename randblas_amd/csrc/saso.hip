@@ -1228,17 +1228,14 @@ __device__ __forceinline__ bool sp_locate(int64_t e, const int64_t *rows, const 
     return sp_locate_rc(rows[e], cols[e], p, v, kk, i);
 }
 
-// entries of virtual row v (v == NV: the scan's closing zero), read by the scan itself
-struct MaskPopcount {
-    const uint32_t *mask;
-    int64_t NV;
-    int mw;   // mask words per virtual row: 2 or 4
-    __device__ __host__ int32_t operator()(int64_t v) const {
-        if (v >= NV) return 0;
-        const uint32_t *m = mask + mw * v;
-        return mw == 2 ? __popc(m[0]) + __popc(m[1]) : __popc(m[0]) + __popc(m[1]) + __popc(m[2]) + __popc(m[3]);
-    }
-};
+// entries of virtual row v: the popcount of its SD_KC / 32 mask words
+__device__ __forceinline__ int32_t row_entries(const uint32_t *mask, int64_t v) {
+    const uint32_t *m = mask + (SD_KC / 32) * v;
+    int32_t c = 0;
+#pragma unroll
+    for (int w = 0; w < SD_KC / 32; ++w) c += __popc(m[w]);
+    return c;
+}
 
 __global__ void mark_kernel(int64_t nnz, const int64_t *rows, const int64_t *cols, const SparseApply p,
                             uint32_t *mask) {
@@ -1250,22 +1247,33 @@ __global__ void mark_kernel(int64_t nnz, const int64_t *rows, const int64_t *col
 
 // records of segment g = (chunk, group of SU_R rows: one wave's rows), padded to a multiple of 4
 // (g == NGT: the scan's closing zero)
-struct SegPadCount {
-    const int32_t *vrp;
-    int64_t M, NG, NGT, R;   // R rows per segment
-    __device__ __host__ int32_t operator()(int64_t g) const {
-        if (g >= NGT) return 0;
-        const int64_t ch = g / NG, r0 = (g % NG) * R;
-        const int64_t r1 = r0 + R < M ? r0 + R : M;
-        return (vrp[ch * M + r1] - vrp[ch * M + r0] + 3) & ~3;
-    }
+// Per virtual row v = (chunk, row i): rowoff[v] = the entries of the rows before i in i's segment
+// (the chunk's rows of i's wave), and the segment's entry count (atomic adds into segcnt).
+__global__ void seg_rows_kernel(int64_t NV, int64_t M, int R, const uint32_t *mask, int32_t *rowoff,
+                                int32_t *segcnt) {
+    const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (v >= NV) return;
+    const int64_t ch = v / M, i = v % M, r0 = i - i % R;
+    const int64_t NG = (M + R - 1) / R;
+    int32_t off = 0;
+    for (int64_t r = r0; r < i; ++r) off += row_entries(mask, ch * M + r);
+    rowoff[v] = off;
+    const int32_t c = row_entries(mask, v);
+    if (c) atomicAdd(&segcnt[ch * NG + i / R], c);
+}
+
+// a segment's record count padded to a multiple of 4 (g == NGT: the scan's closing zero)
+struct SegPad {
+    const int32_t *segcnt;
+    int64_t NGT;
+    __device__ __host__ int32_t operator()(int64_t g) const { return g < NGT ? (segcnt[g] + 3) & ~3 : 0; }
 };
 
 // An entry's record goes to its segment's start + the entries of the segment's earlier rows + its
 // rank in its row (ascending k).
 template <typename T>
 __global__ void place_kernel(int64_t nnz, const int64_t *rows, const int64_t *cols, const T *vals, const SparseApply p,
-                             const uint32_t *mask, const int32_t *vrp, const int32_t *seg, uint32_t *rec,
+                             const uint32_t *mask, const int32_t *rowoff, const int32_t *seg, uint32_t *rec,
                              uint32_t kmul, int R) {
     const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     int64_t v, i;
@@ -1276,7 +1284,7 @@ __global__ void place_kernel(int64_t nnz, const int64_t *rows, const int64_t *co
     for (uint32_t w = 0; w < kk / 32; ++w) rank += __popc(mw[w]);
     const int64_t ch = (v - i) / p.M, grp = i / R;
     const int64_t NG = (p.M + R - 1) / R;
-    const int64_t pos = seg[ch * NG + grp] + (vrp[v] - vrp[ch * p.M + grp * R]) + rank;
+    const int64_t pos = seg[ch * NG + grp] + rowoff[v] + rank;
     const uint32_t row = (uint32_t)(i % R);
     const T x = (T)p.alpha * vals[e];
     rec[pos] = (sizeof(T) == 8 ? 2u * row : row) | ((kk * kmul) << 8) | (signbit(x) ? 0x80000000u : 0u);
@@ -1299,28 +1307,27 @@ static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, co
     const int64_t NGT = nchunks * NG;
     const size_t nrec = n + 3 * (size_t)NGT + 256;   // + segment padding + window / copy overrun (<= 255)
     if (nrec >= (size_t)0x7fffffff) return hipErrorNotSupported;   // int32 record offsets
-    const MaskPopcount pc0{nullptr, NV, mw};
-    auto cnt_it0 = rocprim::make_transform_iterator(rocprim::counting_iterator<int64_t>(0), pc0);
-    size_t scan_bytes = 0, scan2_bytes = 0;
-    hipError_t err = rocprim::exclusive_scan(nullptr, scan_bytes, cnt_it0, (int32_t *)nullptr, 0, (size_t)(NV + 1),
-                                             rocprim::plus<int32_t>(), s);
-    if (err != hipSuccess) return err;
-    const SegPadCount sp0{nullptr, p.M, NG, NGT, R};
+    size_t scan_bytes = 0;
+    hipError_t err;
+    const SegPad sp0{nullptr, NGT};
     auto seg_it0 = rocprim::make_transform_iterator(rocprim::counting_iterator<int64_t>(0), sp0);
-    err = rocprim::exclusive_scan(nullptr, scan2_bytes, seg_it0, (int32_t *)nullptr, 0, (size_t)(NGT + 1),
+    err = rocprim::exclusive_scan(nullptr, scan_bytes, seg_it0, (int32_t *)nullptr, 0, (size_t)(NGT + 1),
                                   rocprim::plus<int32_t>(), s);
     if (err != hipSuccess) return err;
-    if (scan2_bytes > scan_bytes) scan_bytes = scan2_bytes;
     const size_t gen_bytes = gen ? n * (2 * sizeof(int64_t) + sizeof(double)) + 64 : 0;
-    const size_t bytes = (size_t)NV * 4 * mw + (size_t)(NV + 1) * sizeof(int32_t) + (size_t)(NGT + 1) * sizeof(int32_t) +
-                         nrec * sizeof(uint32_t) + scan_bytes + gen_bytes + 256;
+    const size_t bytes = (size_t)NV * 4 * mw + (size_t)NGT * sizeof(int32_t) + (size_t)NV * sizeof(int32_t) +
+                         (size_t)(NGT + 1) * sizeof(int32_t) + nrec * sizeof(uint32_t) + scan_bytes + gen_bytes + 512;
     char *ws = nullptr;
     err = ws_alloc((void **)&ws, bytes, s);
     if (err != hipSuccess) return err;
     size_t off = 0;
     auto carve = [&](size_t b) { void *q = ws + off; off += (b + 15) & ~(size_t)15; return q; };
-    uint32_t *mask = (uint32_t *)carve((size_t)NV * 4 * mw);
-    int32_t *vrp = (int32_t *)carve((size_t)(NV + 1) * sizeof(int32_t));
+    // mask and segcnt adjacent: one memset clears both
+    const size_t mask_b = (size_t)NV * 4 * mw;
+    uint32_t *mask = (uint32_t *)ws;
+    int32_t *segcnt = (int32_t *)(ws + mask_b);
+    off = (mask_b + (size_t)NGT * sizeof(int32_t) + 15) & ~(size_t)15;
+    int32_t *rowoff = (int32_t *)carve((size_t)NV * sizeof(int32_t));
     int32_t *seg = (int32_t *)carve((size_t)(NGT + 1) * sizeof(int32_t));
     uint32_t *rec = (uint32_t *)carve(nrec * sizeof(uint32_t));
     void *tmp = carve(scan_bytes);
@@ -1331,7 +1338,7 @@ static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, co
         rows = gr; cols = gc; vals = gv;
     }
     const uint32_t kmul = y_k ? (uint32_t)sizeof(double) : (uint32_t)(SU_J * sizeof(double));
-    err = hipMemsetAsync(mask, 0, (size_t)NV * 4 * mw, s);
+    err = hipMemsetAsync(mask, 0, mask_b + (size_t)NGT * sizeof(int32_t), s);
     if (err == hipSuccess) err = hipMemsetD32Async(rec, (int)SdCfg::PAD, nrec, s);   // padding records
     if (err == hipSuccess && gen) {
         err = launch_fill_sparse_t<double>(*gen, (int64_t *)rows, (int64_t *)cols, (double *)vals, s, &p, mask);
@@ -1339,19 +1346,19 @@ static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, co
         hipLaunchKernelGGL(mark_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, rows, cols, p, mask);
         err = hipGetLastError();
     }
-    if (err == hipSuccess) {
-        const MaskPopcount pc{mask, NV, mw};
-        auto cnt_it = rocprim::make_transform_iterator(rocprim::counting_iterator<int64_t>(0), pc);
-        err = rocprim::exclusive_scan(tmp, scan_bytes, cnt_it, vrp, 0, (size_t)(NV + 1), rocprim::plus<int32_t>(), s);
+    if (err == hipSuccess && NV > 0) {
+        hipLaunchKernelGGL(seg_rows_kernel, dim3((unsigned)((NV + 255) / 256)), dim3(256), 0, s, NV, p.M, (int)R, mask,
+                           rowoff, segcnt);
+        err = hipGetLastError();
     }
-    if (err == hipSuccess) {
-        const SegPadCount sp{vrp, p.M, NG, NGT, R};
+    if (err == hipSuccess) {   // segment starts: one scan over the (chunk, wave rows) segments
+        const SegPad sp{segcnt, NGT};
         auto seg_it = rocprim::make_transform_iterator(rocprim::counting_iterator<int64_t>(0), sp);
         err = rocprim::exclusive_scan(tmp, scan_bytes, seg_it, seg, 0, (size_t)(NGT + 1), rocprim::plus<int32_t>(), s);
     }
     if (err == hipSuccess && nnz > 0) {
         hipLaunchKernelGGL(place_kernel<double>, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, rows, cols,
-                           vals, p, mask, vrp, seg, rec, kmul, (int)R);
+                           vals, p, mask, rowoff, seg, rec, kmul, (int)R);
         err = hipGetLastError();
     }
     if (err == hipSuccess) {
