@@ -137,12 +137,8 @@ struct GenTileFast {
             const int c = tid + u * NT;
             if (KIND == GEN_OK) {
                 const int o = c / (BK / 4), q = c % (BK / 4);
-#ifdef RBH_ABLATE_GEN
-                for (int e = 0; e < 4; ++e) v[u][e] = (T)(int)((o0 + o + k0 + q + e) & 7);   // diagnostics only
-#else
                 gen_call<T, FAMILY>(g, (uint64_t)(g.pr0 + o0 + o) * g.stride + (uint64_t)((g.pc0 + k0) >> 2) + q,
                                     v[u], tab);
-#endif
                 const bool orow = (o0 + o) < nO;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) v[u][e] = (orow && k0 + 4 * q + e < K) ? v[u][e] : (T)0;
@@ -518,45 +514,34 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void skge_fused_kernel(cons
 }
 
 // ------------------------------------------------------------------------------------------
-// f64 wide tile: 64 generated x 512 memory outer indices, memory operand by LDS-DMA
+// f64 wide tile: 64 generated x 512 memory outer indices
 // ------------------------------------------------------------------------------------------
 // With f64 MFMAs the draw's VALU work does not hide under the matrix pipe, so what the draw costs
 // is set by how often each operator entry is regenerated: once per tile along the memory
 // operand's outer dimension. A 64 x 512 tile draws each entry half as often as 128 x 256 for the
-// same accumulator budget (128 VGPRs per lane). The 512-row memory tile (64 KB per K step) would
-// need 32 staging VGPRs per lane, so it is copied global -> LDS with global_load_lds_dwordx4
-// instead: rows of 16 doubles, unpadded, 16-B vectors XOR-swizzled by (row >> 1) & 7 through the
-// source address, which leaves the fragment reads 2-way banked (the minimum for 128-B rows).
-// Waves 0-3 draw the 64 x 16 generated tile (one Philox call per lane) into padded LDS rows; waves
-// w and w + 4 share a SIMD, so every SIMD carries one drawing wave.
+// same accumulator budget (128 VGPRs per lane). The 512-row memory tile (64 KB per K step) is
+// staged through registers in two halves of 4 x 16 B per lane (the second loaded mid-step) into
+// unpadded rows of 16 doubles, 16-B vectors XOR-swizzled by (row >> 1) & 7, which leaves the
+// fragment reads 2-way banked (the minimum for 128-B rows). (An LDS-DMA copy of the same image
+// measured slower.) Waves 0-3 draw the 64 x 16 generated tile (one Philox call per lane) into
+// padded LDS rows; waves w and w + 4 share a SIMD, so every SIMD carries one drawing wave.
+// Split-K (p.splitk > 1) for grids too small to fill the chip: partial sums to p.partial.
 // Requires K % 16 == 0, a mode-2 memory operand and pc0 % 4 == 0.
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 
-#ifndef RBH_WIDE_WG
-#define RBH_WIDE_WG 1
-#endif
-#ifndef RBH_WIDE_IL
-#define RBH_WIDE_IL 0
-#endif
-#ifndef RBH_WIDE_IL_V
-#define RBH_WIDE_IL_V 4
-#endif
-#ifndef RBH_WIDE_DRAW_AT
-#define RBH_WIDE_DRAW_AT -1   // sub-step after whose MFMAs the drawing waves draw (-1: before the first)
-#endif
 // TRI != 0: the memory operand is a symmetric matrix of which only one triangle is read
 // (sketch_symmetric, sksy.hh:165-537, with A's other triangle never touched). In the operand's own
 // coordinates (o, k) the stored triangle is k <= o (TRI 1 full storage, 3 packed) or k >= o (2, 4);
 // element (o, k) outside it is the stored (k, o). A K step's 512 x 16 tile is then wholly inside
 // the triangle (loaded as usual), wholly outside (loaded from the mirror tile, which is contiguous
 // along o, and transposed into the LDS image), or straddles the diagonal (per-element select).
-template <int GK, int FAMILY, bool GX, int TRI = 0>
+template <int GK, int FAMILY, bool GX, int TRI, bool SPLIT>
 __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
     typedef double T;
     // 8 waves = WGW (along the generated dimension) x WMW (along the memory dimension); each wave
     // holds FA x FB MFMA tiles of 16 x 16 (FA * FB = 16: 128 accumulator VGPRs)
-    constexpr int WGW = RBH_WIDE_WG, WMW = 8 / WGW;
+    constexpr int WGW = 1, WMW = 8 / WGW;
     constexpr int BG = 64, BMM = 512;
     constexpr int FA = BG / 16 / WGW, FB = BMM / 16 / WMW;
     constexpr int LDG = BK + 2;
@@ -577,30 +562,17 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
     const MemOperand &mop = GX ? p.ym : p.xm;
     const int64_t gnO = GX ? p.M : p.N, mnO = GX ? p.N : p.M;
     const int64_t nTg = (gnO + BG - 1) / BG, nTm = (mnO + BMM - 1) / BMM;
-    const int64_t nb = nTg * nTm;
+    const int split = SPLIT ? p.splitk : 1;   // (SPLIT = false keeps the unsplit loop's bounds constant)
+    const int64_t nb = nTg * nTm * split;
     const int64_t b = blockIdx.x;
     const int64_t xcd = b % 8, qq = nb / 8, rr = nb % 8;
-    const int64_t t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + b / 8;
+    const int64_t t_all = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + b / 8;
+    const int64_t z = t_all % split, t = t_all / split;   // the K splits of a tile run side by side
     const int64_t go0 = (t % nTg) * BG, mo0 = (t / nTg) * BMM;
 
-    // LDS-DMA of the memory tile for step k0 into stage st: this wave's 8 pieces of 8 rows
     const T *mptr = (const T *)mop.ptr;
-    const int drow = lane >> 3, dslot = lane & 7;
-    auto dma = [&](int64_t k0, int st) {
-        const int64_t ck0 = k0 < p.K ? k0 : p.K - BK;   // past K (last step's prefetch): any valid address
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int blk = 8 * wave + i;
-            const int o = 8 * blk + drow;
-            const int v = dslot ^ ((o >> 1) & 7);
-            int64_t go = mo0 + o;
-            go = go < mnO ? go : mnO - 1;
-            const T *src = mptr + go * mop.so + ck0 + 2 * v;
-            __builtin_amdgcn_global_load_lds((glb_void_t *)src, (lds_void_t *)(lds + st * MS + blk * 128), 16, 0, 0);
-        }
-    };
-    // register staging (default; RBH_WIDE_DMA selects the LDS-DMA above): the same swizzled image,
-    // written with ds_write_b128 from two 4-vector halves, the second half loaded mid-step.
+    // register staging: the swizzled image, written with ds_write_b128 from two 4-vector halves, the
+    // second half loaded mid-step.
     // Thread tid stages vectors idx = tid + 512 * e (e < 8): row o = (tid >> 3) + 64 * e, 16-B
     // vector v = tid & 7, LDS slot v ^ ((o >> 1) & 7) = v ^ ((tid >> 4) & 7), the same for every e.
     // Everything per lane is loop-invariant: per step only the uniform k offset moves (SGPR base
@@ -722,20 +694,12 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
             }
             rb::ctr_add(gop.ctr, off, c);
         }
-#ifdef RBH_ABLATE_GEN
-        for (int e = 0; e < 4; ++e) gv[e] = (T)(int)((c[0] + e) & 7);   // diagnostics only
-#else
         const rb::u32x4 w = rb::philox4x32<10>(c[0], c[1], c[2], c[3], gop.key[0], gop.key[1]);
         float sm[4];
         rb::sample4<FAMILY>(w, sm, tab);
 #pragma unroll
         for (int e = 0; e < 4; ++e) gv[e] = FAMILY == rb::UNIFORM ? (T)sm[e] * (T)gop.scale : (T)sm[e];
-#endif
-#if RBH_WIDE_IL
-        {   // branch-free (the draw shares its basic block with the MFMAs): edge masks as selects
-#else
         if (!gtile_full || kt * BK >= p.K) {   // uniform: edge tile or the prefetch past K
-#endif
             if (GK == GEN_OK) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) gv[e] = (glane_ok && kt * BK < p.K) ? gv[e] : (T)0;
@@ -765,55 +729,41 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
 #pragma unroll
         for (int c = 0; c < FB; ++c) acc[a][c] = (acc_t){0, 0, 0, 0};
 
+    // K steps [kt0, kt1) of this workgroup's split (split-K: p.splitk > 1)
     const int64_t nk = p.K / BK;
+    const int64_t per = SPLIT ? (nk + split - 1) / split : nk;
+    const int64_t kt0 = SPLIT ? z * per : 0, kt1 = SPLIT ? (kt0 + per < nk ? kt0 + per : nk) : nk;
     __syncthreads();   // tab
-#ifndef RBH_WIDE_DMA
     if (TRI) {
-        const int c0 = tclass(0);
-        rload_tri(0, 0, c0); rstore_tri(0, 0, c0); rload_tri(0, 1, c0); rstore_tri(0, 1, c0);
+        const int c0 = tclass(kt0 * BK);
+        rload_tri(kt0 * BK, 0, c0); rstore_tri(0, 0, c0); rload_tri(kt0 * BK, 1, c0); rstore_tri(0, 1, c0);
     } else {
-        rload(0, 0); rstore(0, 0); rload(0, 1); rstore(0, 1);
+        rload(kt0 * BK, 0); rstore(0, 0); rload(kt0 * BK, 1); rstore(0, 1);
     }
-#else
-    dma(0, 0);
-#endif
-    if (wave < 4) { draw(0); gstore(0); }
+    if (wave < 4) { draw(kt0); gstore(0); }
     __syncthreads();
 
     // fragment addresses (doubles) relative to the stage base
     const int gfa = (16 * FA * wg + r) * LDG + 4 * g;   // + 16 * a * LDG per fragment a
     const int mrow = (16 * FB * wmm + r) * BK;          // + 16 * c * BK per fragment c
     const int msw = (r >> 1) & 7;
-    // RBH_WIDE_IL: 0 = the drawing waves draw in a branch ahead of their MFMAs; 1 = two copies of
-    // the loop (drawing / not drawing waves), the draw in the MFMAs' basic block; 2 = as 1, with
-    // the drawing waves' MFMAs and draw VALU interleaved by sched_group_barrier
-    auto k_loop = [&](auto drawer_tag) {
-    constexpr bool DRAWER = decltype(drawer_tag)::value;
-    for (int64_t kt = 0; kt < nk; ++kt) {
-        const int cur = (int)(kt & 1);
+    // (the loop as a lambda: measured 9.25 -> 8.93 ms at C2 against the same loop written inline)
+    auto k_loop = [&]() {
+    for (int64_t kt = kt0; kt < kt1; ++kt) {
+        const int cur = (int)((kt - kt0) & 1);
         const T *Mc = lds + cur * MS;
         const T *Gc = lds + 2 * MS + cur * GS;
         const int64_t kn = (kt + 1) * BK;
         const int cn = tclass(kn);
-#ifndef RBH_WIDE_DMA
         if (TRI) rload_tri(kn, 0, cn);
         else rload(kn, 0);
-#else
-        dma(kn, cur ^ 1);
-#endif
-#if RBH_WIDE_IL
-        if (DRAWER) draw(kt + 1);
-#else
-        if (RBH_WIDE_DRAW_AT < 0 && wave < 4) draw(kt + 1);
-#endif
+        if (wave < 4) draw(kt + 1);
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-#ifndef RBH_WIDE_DMA
             if (s == 2) {
                 if (TRI) { rstore_tri(cur ^ 1, 0, cn); rload_tri(kn, 1, cn); }
                 else { rstore(cur ^ 1, 0); rload(kn, 1); }
             }
-#endif
             T gf[FA];
 #pragma unroll
             for (int a = 0; a < FA; ++a) gf[a] = Gc[gfa + 16 * a * LDG + s];
@@ -826,43 +776,20 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
 #pragma unroll
                 for (int c = 0; c < FB; ++c)
                     acc[a][c] = GX ? Mfma<T>::mma(mf[c], gf[a], acc[a][c]) : Mfma<T>::mma(gf[a], mf[c], acc[a][c]);
-#if !RBH_WIDE_IL
-            if (s == RBH_WIDE_DRAW_AT && wave < 4) draw(kt + 1);   // after this sub-step's MFMAs are issued
-#endif
-#ifdef RBH_WIDE_SB
-            __builtin_amdgcn_sched_barrier(0);
-#endif
         }
-#if RBH_WIDE_IL
-        if (DRAWER) gstore(cur ^ 1);
-#else
         if (wave < 4) gstore(cur ^ 1);
-#endif
-#ifndef RBH_WIDE_DMA
         if (TRI) rstore_tri(cur ^ 1, 1, cn);
         else rstore(cur ^ 1, 1);
-#endif
-#if RBH_WIDE_IL == 2
-        if (DRAWER) {
-#pragma unroll
-            for (int q = 0; q < 4 * FA * FB; ++q) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);              // one MFMA
-                __builtin_amdgcn_sched_group_barrier(0x002, RBH_WIDE_IL_V, 0);  // then draw VALU
-            }
-        }
-#endif
         __syncthreads();
     }
     };
-#if RBH_WIDE_IL
-    if (wave < 4) k_loop(std::true_type{});
-    else k_loop(std::false_type{});
-#else
-    k_loop(std::false_type{});
-#endif
+    k_loop();
 
-    T *C = (T *)p.C;
-    const T alpha = (T)p.alpha, beta = (T)p.beta;
+    // split-K: alpha times this split's partial sum to partial[z] (M x N col-major); the reduction
+    // adds the splits in order and applies beta
+    T *C = SPLIT ? (T *)p.partial + z * p.M * p.N : (T *)p.C;
+    const int64_t ldc = SPLIT ? p.M : p.ldc;
+    const T alpha = (T)p.alpha, beta = SPLIT ? (T)0 : (T)p.beta;
 #pragma unroll
     for (int a = 0; a < FA; ++a)
 #pragma unroll
@@ -874,7 +801,7 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
             const int64_t i = GX ? gi + r : mi + r;
             const int64_t j = GX ? mi + dr : gi + dr;
             if (i < p.M && j < p.N) {
-                T *dst = C + i + j * p.ldc;
+                T *dst = C + i + j * ldc;
                 const T v = alpha * acc[a][c][reg];
                 *dst = (beta == (T)0) ? v : v + beta * *dst;
             }
@@ -919,20 +846,39 @@ static hipError_t launch_one(const GemmProblem &p, hipStream_t s) {
     return e;
 }
 
+constexpr int64_t SPLIT_TILES = 128;   // fewer output tiles than this: split K ...
+constexpr int64_t SPLIT_MIN_NK = 128;  // ... when K has at least this many steps (K >= 2048). A split
+                                       // sum rounds differently from the unsplit kernels (within the
+                                       // tolerance of every dense parity test); below this K every
+                                       // kernel adds in the same order, so layouts agree bitwise
+
+// split-K factor: 1, or enough splits to give 256 workgroups when the output tiles alone cannot
+// fill the chip (C1: d = 128, n = 4096, 16 wide tiles, split 16), each split keeping at least 16 K
+// steps; RBH_SPLITK = s forces s. Deterministic: the splits are added in order by the reduction.
+static int choose_split(int64_t tiles, int64_t nk) {
+    static const int split_env = [] { const char *e = getenv("RBH_SPLITK"); return e ? atoi(e) : 0; }();
+    int split = 1;
+    if (split_env > 0) split = split_env;
+    else if (tiles < SPLIT_TILES && nk >= SPLIT_MIN_NK) {
+        const int64_t want = (256 + tiles - 1) / tiles, most = nk / 16;
+        split = (int)(want < most ? want : most);
+    }
+    if (split > nk) split = (int)nk;
+    return split < 1 ? 1 : split;
+}
+
+
 template <typename T, int XK, int YK, int FAMILY, int BM, int BN, int WMS, int WNS>
 static hipError_t launch_fused(const GemmProblem &p, hipStream_t s) {
     const int64_t nb = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
     if (nb <= 0) return hipSuccess;
     // two LDS stages of (BM + BN) rows: 17-element f64 rows keep the 64 x 512 tile under 160 KB
     constexpr int LDK = (sizeof(T) == 8 && BM + BN > 384) ? BK + 1 : Mfma<T>::LDK;
-    // Optional split-K (RBH_SPLITK = s > 1): s workgroups per tile each take 1/s of K and a
-    // deterministic reduction forms C. Measured at C4 (256 workgroups, one per CU): 6.08 ms
-    // unsplit, 6.11 / 6.14 ms with 2 / 4 splits, so it is off by default.
-    static const int split_env = [] { const char *e = getenv("RBH_SPLITK"); return e ? atoi(e) : 0; }();
+    // Split-K (choose_split): s workgroups per tile each take 1/s of K and a deterministic reduction
+    // forms C. Measured at C4 (256 workgroups, one per CU): 6.08 ms unsplit, 6.11 / 6.14 ms with
+    // 2 / 4 splits forced, so a full grid stays unsplit.
     const int64_t nk = (p.K + BK - 1) / BK;
-    int split = 1;
-    if (split_env > 0) split = split_env;
-    if (split > nk) split = (int)(nk > 0 ? nk : 1);
+    const int split = choose_split(nb, nk);
     GemmProblem q = p;
     q.splitk = split;
     q.partial = nullptr;
@@ -971,13 +917,33 @@ static bool fused_ok(const GemmProblem &p) {
 
 template <int GK, int FAMILY, bool GX, int TRI = 0>
 static hipError_t launch_wide(const GemmProblem &p, hipStream_t s) {
+    typedef double T;
     const int64_t gnO = GX ? p.M : p.N, mnO = GX ? p.N : p.M;
     const int64_t nb = ((gnO + 63) / 64) * ((mnO + 511) / 512);
     if (nb <= 0) return hipSuccess;
+    const int split = choose_split(nb, p.K / BK);
+    GemmProblem q = p;
+    q.splitk = split;
+    q.partial = nullptr;
+    hipError_t e;
+    if (split > 1) {
+        e = ws_alloc(&q.partial, sizeof(T) * (size_t)split * p.M * p.N, s);
+        if (e != hipSuccess) return e;
+    }
     timing_begin(s);
-    hipLaunchKernelGGL((skge_wide_kernel<GK, FAMILY, GX, TRI>), dim3((unsigned)nb), dim3(512), 0, s, p);
-    hipError_t e = hipGetLastError();
+    if (split > 1) hipLaunchKernelGGL((skge_wide_kernel<GK, FAMILY, GX, TRI, true>), dim3((unsigned)(nb * split)), dim3(512), 0, s, q);
+    else hipLaunchKernelGGL((skge_wide_kernel<GK, FAMILY, GX, TRI, false>), dim3((unsigned)nb), dim3(512), 0, s, q);
+    e = hipGetLastError();
+    if (split > 1 && e == hipSuccess) {
+        hipLaunchKernelGGL(splitk_reduce_kernel<T>, dim3(2048), dim3(256), 0, s, p.M, p.N, split,
+                           (const T *)q.partial, (T)p.beta, (T *)p.C, p.ldc);
+        e = hipGetLastError();
+    }
     timing_end(s);
+    if (split > 1) {
+        const hipError_t e2 = ws_free(q.partial, s);
+        if (e == hipSuccess) e = e2;
+    }
     return e;
 }
 
