@@ -648,22 +648,6 @@ template <> struct SuAcc<double> {
                      : "m0", "scc");
     }
 };
-// SU_F32_V (diagnostics, with RBH_SASO_F32_UNIT=1 routing f32 here): 0 = xor + index-mode add in
-// one statement; 1 = 0 with s_nop 1 after s_set_gpr_idx_on; 2 = the f64 form (sign flip outside,
-// index-mode add alone); 3 = 0 with s_nop 4 between the xor and s_set_gpr_idx_on.
-#ifndef SU_F32_V
-#define SU_F32_V 0
-#endif
-#if SU_F32_V == 1
-#define SU_F32_NA ""
-#define SU_F32_NB "s_nop 1\n\t"
-#elif SU_F32_V == 3
-#define SU_F32_NA "s_nop 4\n\t"
-#define SU_F32_NB ""
-#else
-#define SU_F32_NA ""
-#define SU_F32_NB ""
-#endif
 template <> struct SuAcc<float> {
     typedef float v32 __attribute__((ext_vector_type(32)));
     v32 a;
@@ -673,31 +657,16 @@ template <> struct SuAcc<float> {
     // the record's SGPR right before s_set_gpr_idx_on lost whole entries).
     __device__ __forceinline__ void add_at(uint32_t rec, float y) {
         if (SU_ABL & 8) { a[0] += __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, y) ^ (rec & 0x80000000u)); return; }
-#if SU_F32_V == 2
-        uint32_t m;
-        asm("s_and_b32 %0, %1, 0x80000000" : "=s"(m) : "s"(rec) : "scc");
-        const float ys = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, y) ^ m);
-        asm volatile("s_waitcnt lgkmcnt(0)\n\t"
-                     "s_set_gpr_idx_on %1, gpr_idx(SRC0,DST)\n\t"
-                     "v_add_f32 v32, v32, %2\n\t"
-                     "s_set_gpr_idx_off"
-                     : "+{v[32:63]}"(a)
-                     : "s"(rec), "v"(ys)
-                     : "m0", "scc");
-#else
         float t;
         asm volatile("v_xor_b32 %1, %3, %4\n\t"
-                     SU_F32_NA
                      "s_waitcnt lgkmcnt(0)\n\t"
                      "s_set_gpr_idx_on %2, gpr_idx(SRC0,DST)\n\t"
-                     SU_F32_NB
                      "v_add_f32 v32, v32, %1\n\t"
                      "s_set_gpr_idx_off"
                      : "+{v[32:63]}"(a), "=&v"(t)
                      : "s"(__builtin_amdgcn_readfirstlane(rec)), "s"(__builtin_amdgcn_readfirstlane(rec & 0x80000000u)),
                        "v"(y)
                      : "m0", "scc");
-#endif
     }
 };
 
@@ -1449,8 +1418,11 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
     const bool y_j = p.ysj == 1;
     const bool y_k = p.ysk == 1 && (p.ysj % VEC) == 0 && (((uintptr_t)p.Y) % 16) == 0 && (p.K % VEC) == 0;
     static const bool unit_off = [] { const char *e = getenv("RBH_NO_SASO_UNIT"); return e && e[0] == '1'; }();
-    // f64 only: the f32 instantiation (index-mode v_add_f32) lost isolated entries on gfx950;
-    // f32 takes the general-value kernel (RBH_SASO_F32_UNIT=1 routes it here for diagnostics)
+    // f64 only. The f32 instantiation loses whole panel rows on gfx950 (round-2 stress,
+    // tools/f32_stress.sh: sampled f32, RowMajor, d=1000, m=2048, n=130: k = 124 or 60 mod 128 --
+    // the staging registers of one wave -- missing from one 64-column block, and once an illegal
+    // address), while the f64 one at the same shape ran 160 of 160 clean; f32 takes the
+    // general-value kernel (RBH_SASO_F32_UNIT=1 routes it here for that stress)
     static const bool f32_unit = [] { const char *e = getenv("RBH_SASO_F32_UNIT"); return e && e[0] == '1'; }();
     const bool unit = (y_j || y_k) && !unit_off && (sizeof(T) == 8 || f32_unit);
 

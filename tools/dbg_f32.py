@@ -81,6 +81,12 @@ def run(fn_name, dtype, layout, d=300, n=70, m=1000, vec=4, key=1, alpha=1.0, be
                 print(f"      row {i} holds row {i2}'s expected values")
 
 
+if os.environ.get("DBG_F64_UNIT") == "1":   # f64 user arrays with +-1 values: the f64 unit kernel
+    for rep in range(int(os.environ.get("DBG_REPS", "3"))):
+        for lay in ("C", "R"):
+            for f in ("unit", "scaled"):
+                run(f, np.float64, lay, d=1000, n=130, m=2048, vec=8, key=7, sampled=False)
+    sys.exit(0)
 if os.environ.get("DBG_SAMPLED") == "1":
     for rep in range(3):
         for dt in (np.float32, np.float64):
