@@ -55,11 +55,16 @@ CONFIGS = {
 }
 
 
+# the timed kernel of each workload kind (its name in the rocprofv3 summaries)
+DOMINANT = {"dense": "skge_", "saso": "saso_dma_kernel", "sksy": "skge_", "sksyp": "skge_"}
+
+
 def pmc_traffic(config):
     """HBM bytes per launch of the dominant kernel, from the committed rocprofv3 PMC summary of this
     config (tools/pmc.sh -> tools/pmc_summary.py -> profiles/<round>/<config>_pmc.json): FETCH_SIZE
     (doubled, the gfx950 correction of MI355X_MICROARCH.md) + WRITE_SIZE. The dominant kernel is the
-    one with the most GRBM_GUI_ACTIVE cycles. None when no summary exists."""
+    config's timed kernel (DOMINANT), the one with the most GRBM_GUI_ACTIVE cycles among those named
+    so (the input preparation, fill_dense of A, is not it). None when no summary exists."""
     import glob
     files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r*",
                                           f"{config}_pmc.json")))
@@ -67,7 +72,10 @@ def pmc_traffic(config):
         return None, None
     with open(files[-1]) as f:
         d = json.load(f)
-    kern = max(d, key=lambda k: d[k].get("GRBM_GUI_ACTIVE", 0.0))
+    named = [k for k in d if DOMINANT[CONFIGS[config][0]] in k]
+    if not named:
+        return None, None
+    kern = max(named, key=lambda k: d[k].get("GRBM_GUI_ACTIVE", 0.0))
     if "hbm_bytes" not in d[kern]:
         return None, None
     rel = os.path.relpath(files[-1], os.path.dirname(os.path.abspath(__file__)))
