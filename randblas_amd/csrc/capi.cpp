@@ -88,15 +88,14 @@ hipError_t ws_alloc(void **p, size_t bytes, hipStream_t s) {
         pool = g_pool[dev];
     }
     // diagnostics (the pool-trim study): RBH_WS_MODE=legacy takes workspaces from
-    // hipMalloc; =sync synchronises the stream after each pool allocation; =zero memsets it
+    // hipMalloc; =sync synchronises the stream after each pool allocation
     static const int mode = [] {
         const char *m = getenv("RBH_WS_MODE");
-        return !m ? 0 : (!strcmp(m, "legacy") ? 1 : (!strcmp(m, "sync") ? 2 : (!strcmp(m, "zero") ? 3 : 0)));
+        return !m ? 0 : (!strcmp(m, "legacy") ? 1 : (!strcmp(m, "sync") ? 2 : 0));
     }();
     if (mode == 1) return hipMalloc(p, bytes);
     e = hipMallocFromPoolAsync(p, bytes, pool, s);
     if (e == hipSuccess && mode == 2) e = hipStreamSynchronize(s);
-    if (e == hipSuccess && mode == 3) e = hipMemsetAsync(*p, 0, bytes, s);
     return e;
 }
 hipError_t ws_free(void *p, hipStream_t s) {
