@@ -9,6 +9,7 @@
 // works unchanged; device arrays are used in place and the work is stream-ordered.
 #include <hip/hip_runtime.h>
 
+#include <map>
 #include <mutex>
 #include <cmath>
 #include <cstdarg>
@@ -61,42 +62,80 @@ void timing_end(hipStream_t s) {
 // block allocated after such a trim was observed to lose a kernel's writes in a C++ client that
 // also stages host arrays through hipMalloc (B read back as zeros; memset of the fresh block then
 // faulted). DESIGN.md §7 records the study; RBH_POOL_KEEP_BYTES overrides the threshold for it.
+//
+// On top of the pool, one arena per (device, stream): workspaces are carved from a block the
+// stream keeps, so a call frees nothing back to the pool. hipFreeAsync blocks the host for about as
+// long as the stream's queued work (measured 0.44 ms per C3 call), which kept the host from running
+// ahead of the GPU; reuse within one stream is safe without it, because the stream orders the work.
+// A request that does not fit grows the arena when it is empty, else takes a plain pool block.
 namespace {
 std::mutex g_pool_mu;
 hipMemPool_t g_pool[64] = {};
+struct Arena {
+    char *base = nullptr;
+    size_t cap = 0;
+    std::vector<std::pair<size_t, size_t>> live;   // (offset, bytes), in allocation order
+    size_t top() const { return live.empty() ? 0 : live.back().first + live.back().second; }
+};
+std::map<std::pair<int, hipStream_t>, Arena> g_arenas;
+
+hipError_t pool_of(int dev, hipMemPool_t *pool) {   // (g_pool_mu held)
+    if (!g_pool[dev]) {
+        hipMemPoolProps props{};
+        props.allocType = hipMemAllocationTypePinned;
+        props.handleTypes = hipMemHandleTypeNone;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = dev;
+        hipError_t e = hipMemPoolCreate(&g_pool[dev], &props);
+        if (e != hipSuccess) { g_pool[dev] = nullptr; return e; }
+        const char *k = getenv("RBH_POOL_KEEP_BYTES");
+        uint64_t keep = k ? strtoull(k, nullptr, 10) : UINT64_MAX;
+        (void)hipMemPoolSetAttribute(g_pool[dev], hipMemPoolAttrReleaseThreshold, &keep);
+    }
+    *pool = g_pool[dev];
+    return hipSuccess;
+}
 }  // namespace
 hipError_t ws_alloc(void **p, size_t bytes, hipStream_t s) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-    hipMemPool_t pool;
-    {
-        std::lock_guard<std::mutex> lk(g_pool_mu);
-        if (!g_pool[dev]) {
-            hipMemPoolProps props{};
-            props.allocType = hipMemAllocationTypePinned;
-            props.handleTypes = hipMemHandleTypeNone;
-            props.location.type = hipMemLocationTypeDevice;
-            props.location.id = dev;
-            e = hipMemPoolCreate(&g_pool[dev], &props);
-            if (e != hipSuccess) { g_pool[dev] = nullptr; return e; }
-            const char *k = getenv("RBH_POOL_KEEP_BYTES");
-            uint64_t keep = k ? strtoull(k, nullptr, 10) : UINT64_MAX;
-            (void)hipMemPoolSetAttribute(g_pool[dev], hipMemPoolAttrReleaseThreshold, &keep);
-        }
-        pool = g_pool[dev];
-    }
     // diagnostics (the pool-trim study): RBH_WS_MODE=legacy takes workspaces from
-    // hipMalloc; =sync synchronises the stream after each pool allocation
+    // hipMalloc; =sync synchronises the stream after each pool allocation (no arena in either)
     static const int mode = [] {
         const char *m = getenv("RBH_WS_MODE");
         return !m ? 0 : (!strcmp(m, "legacy") ? 1 : (!strcmp(m, "sync") ? 2 : 0));
     }();
     if (mode == 1) return hipMalloc(p, bytes);
-    e = hipMallocFromPoolAsync(p, bytes, pool, s);
-    if (e == hipSuccess && mode == 2) e = hipStreamSynchronize(s);
-    return e;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    hipMemPool_t pool;
+    e = pool_of(dev, &pool);
+    if (e != hipSuccess) return e;
+    if (mode == 2) {
+        e = hipMallocFromPoolAsync(p, bytes, pool, s);
+        return e == hipSuccess ? hipStreamSynchronize(s) : e;
+    }
+    const size_t need = (bytes + 255) & ~(size_t)255;
+    Arena &a = g_arenas[{dev, s}];
+    if (a.base && a.top() + need <= a.cap) {
+        a.live.emplace_back(a.top(), need);
+        *p = a.base + a.live.back().first;
+        return hipSuccess;
+    }
+    if (a.live.empty()) {   // grow: the old block is released in stream order
+        const size_t cap = need > 2 * a.cap ? need : 2 * a.cap;
+        char *nb = nullptr;
+        e = hipMallocFromPoolAsync((void **)&nb, cap, pool, s);
+        if (e != hipSuccess) return e;
+        if (a.base) (void)hipFreeAsync(a.base, s);
+        a.base = nb;
+        a.cap = cap;
+        a.live.emplace_back(0, need);
+        *p = a.base;
+        return hipSuccess;
+    }
+    return hipMallocFromPoolAsync(p, bytes, pool, s);
 }
 hipError_t ws_free(void *p, hipStream_t s) {
     static const bool legacy = [] { const char *m = getenv("RBH_WS_MODE"); return m && !strcmp(m, "legacy"); }();
@@ -104,6 +143,19 @@ hipError_t ws_free(void *p, hipStream_t s) {
     if (legacy) {
         hipError_t e = hipStreamSynchronize(s);
         return e == hipSuccess ? hipFree(p) : e;
+    }
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        auto it = g_arenas.find({dev, s});
+        if (it != g_arenas.end() && it->second.base && (char *)p >= it->second.base &&
+            (char *)p < it->second.base + it->second.cap) {
+            Arena &a = it->second;
+            const size_t off = (size_t)((char *)p - a.base);
+            for (size_t i = a.live.size(); i-- > 0;)
+                if (a.live[i].first == off) { a.live.erase(a.live.begin() + (ptrdiff_t)i); break; }
+            return hipSuccess;
+        }
     }
     return hipFreeAsync(p, s);
 }

@@ -1216,19 +1216,58 @@ __global__ void mark_kernel(int64_t nnz, const int64_t *rows, const int64_t *col
 
 // records of segment g = (chunk, group of SU_R rows: one wave's rows), padded to a multiple of 4
 // (g == NGT: the scan's closing zero)
-// Per virtual row v = (chunk, row i): rowoff[v] = the entries of the rows before i in i's segment
-// (the chunk's rows of i's wave), and the segment's entry count (atomic adds into segcnt).
-__global__ void seg_rows_kernel(int64_t NV, int64_t M, int R, const uint32_t *mask, int32_t *rowoff,
-                                int32_t *segcnt) {
-    const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (v >= NV) return;
-    const int64_t ch = v / M, i = v % M, r0 = i - i % R;
-    const int64_t NG = (M + R - 1) / R;
-    int32_t off = 0;
-    for (int64_t r = r0; r < i; ++r) off += row_entries(mask, ch * M + r);
-    rowoff[v] = off;
-    const int32_t c = row_entries(mask, v);
-    if (c) atomicAdd(&segcnt[ch * NG + i / R], c);
+// Per segment g = (chunk, R = 32 rows): 32 lanes take its rows, a segmented scan over the half
+// wave gives each row's offset inside the segment (rowoff[v], v = (chunk, row)) and the segment's
+// entry count (segcnt[g], written by its last lane).
+__global__ __launch_bounds__(256) void seg_rows_kernel(int64_t NGT, int64_t NG, int64_t M, const uint32_t *mask,
+                                                       int32_t *rowoff, int32_t *segcnt) {
+    static_assert(SU_R == 32, "one half wave per segment");
+    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int64_t g = t / SU_R;
+    const int l = (int)(t % SU_R);
+    const int64_t ch = g / NG, r = (g % NG) * SU_R + l;
+    const bool in = g < NGT && r < M;
+    const int64_t v = ch * M + r;
+    const int32_t c = in ? row_entries(mask, v) : 0;
+    int32_t x = c;   // inclusive scan over the 32 lanes of this segment (aligned half wave)
+#pragma unroll
+    for (int o = 1; o < SU_R; o <<= 1) {
+        const int32_t y = __shfl_up(x, o, SU_R);
+        if (l >= o) x += y;
+    }
+    if (in) rowoff[v] = x - c;
+    if (g < NGT && l == SU_R - 1) segcnt[g] = x;
+}
+
+// Exclusive scan of the padded segment counts in one workgroup (NGT + 1 <= SEG_SCAN_MAX): each
+// thread sums SEG_SCAN_PT consecutive counts, the wave and workgroup scans give its offset.
+constexpr int SEG_SCAN_NT = 1024, SEG_SCAN_PT = 16, SEG_SCAN_MAX = SEG_SCAN_NT * SEG_SCAN_PT;
+__global__ __launch_bounds__(SEG_SCAN_NT) void seg_scan_small_kernel(int64_t NGT, const int32_t *segcnt, int32_t *seg) {
+    __shared__ int32_t wsum[SEG_SCAN_NT / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t b0 = (int64_t)tid * SEG_SCAN_PT;
+    int32_t c[SEG_SCAN_PT], t = 0;
+#pragma unroll
+    for (int q = 0; q < SEG_SCAN_PT; ++q) {
+        c[q] = b0 + q < NGT ? (segcnt[b0 + q] + 3) & ~3 : 0;
+        t += c[q];
+    }
+    int32_t x = t;   // inclusive scan over the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    int32_t base = 0;
+    for (int w = 0; w < wave; ++w) base += wsum[w];
+    int32_t run = base + x - t;   // exclusive offset of this thread's first element
+#pragma unroll
+    for (int q = 0; q < SEG_SCAN_PT; ++q) {
+        if (b0 + q <= NGT) seg[b0 + q] = run;   // seg[NGT] = the total
+        run += c[q];
+    }
 }
 
 // a segment's record count padded to a multiple of 4 (g == NGT: the scan's closing zero)
@@ -1242,8 +1281,8 @@ struct SegPad {
 // rank in its row (ascending k).
 template <typename T>
 __global__ void place_kernel(int64_t nnz, const int64_t *rows, const int64_t *cols, const T *vals, const SparseApply p,
-                             const uint32_t *mask, const int32_t *rowoff, const int32_t *seg, uint32_t *rec,
-                             uint32_t kmul, int R) {
+                             const uint32_t *mask, const int32_t *rowoff, const int32_t *segcnt, const int32_t *seg,
+                             uint32_t *rec, uint32_t kmul, int R, uint32_t pad) {
     const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     int64_t v, i;
     uint32_t kk;
@@ -1253,10 +1292,14 @@ __global__ void place_kernel(int64_t nnz, const int64_t *rows, const int64_t *co
     for (uint32_t w = 0; w < kk / 32; ++w) rank += __popc(mw[w]);
     const int64_t ch = (v - i) / p.M, grp = i / R;
     const int64_t NG = (p.M + R - 1) / R;
-    const int64_t pos = seg[ch * NG + grp] + rowoff[v] + rank;
+    const int64_t g = ch * NG + grp;
+    const int32_t at = rowoff[v] + (int32_t)rank;   // position inside the segment
+    const int64_t pos = seg[g] + at;
     const uint32_t row = (uint32_t)(i % R);
     const T x = (T)p.alpha * vals[e];
     rec[pos] = (sizeof(T) == 8 ? 2u * row : row) | ((kk * kmul) << 8) | (signbit(x) ? 0x80000000u : 0u);
+    if (at == segcnt[g] - 1)   // the segment's last entry pads it to a multiple of four
+        for (int64_t q = pos + 1; q < seg[g + 1]; ++q) rec[q] = pad;
 }
 
 // The LDS-DMA apply (section 5) on a sort-free CSR. With gen, the operator is sampled here into
@@ -1291,11 +1334,9 @@ static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, co
     if (err != hipSuccess) return err;
     size_t off = 0;
     auto carve = [&](size_t b) { void *q = ws + off; off += (b + 15) & ~(size_t)15; return q; };
-    // mask and segcnt adjacent: one memset clears both
     const size_t mask_b = (size_t)NV * 4 * mw;
-    uint32_t *mask = (uint32_t *)ws;
-    int32_t *segcnt = (int32_t *)(ws + mask_b);
-    off = (mask_b + (size_t)NGT * sizeof(int32_t) + 15) & ~(size_t)15;
+    uint32_t *mask = (uint32_t *)carve(mask_b);
+    int32_t *segcnt = (int32_t *)carve((size_t)NGT * sizeof(int32_t));
     int32_t *rowoff = (int32_t *)carve((size_t)NV * sizeof(int32_t));
     int32_t *seg = (int32_t *)carve((size_t)(NGT + 1) * sizeof(int32_t));
     uint32_t *rec = (uint32_t *)carve(nrec * sizeof(uint32_t));
@@ -1307,27 +1348,29 @@ static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, co
         rows = gr; cols = gc; vals = gv;
     }
     const uint32_t kmul = y_k ? (uint32_t)sizeof(double) : (uint32_t)(SU_J * sizeof(double));
-    err = hipMemsetAsync(mask, 0, mask_b + (size_t)NGT * sizeof(int32_t), s);
-    if (err == hipSuccess) err = hipMemsetD32Async(rec, (int)SdCfg::PAD, nrec, s);   // padding records
+    err = hipMemsetAsync(mask, 0, mask_b, s);
     if (err == hipSuccess && gen) {
         err = launch_fill_sparse_t<double>(*gen, (int64_t *)rows, (int64_t *)cols, (double *)vals, s, &p, mask);
     } else if (err == hipSuccess && nnz > 0) {
         hipLaunchKernelGGL(mark_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, rows, cols, p, mask);
         err = hipGetLastError();
     }
-    if (err == hipSuccess && NV > 0) {
-        hipLaunchKernelGGL(seg_rows_kernel, dim3((unsigned)((NV + 255) / 256)), dim3(256), 0, s, NV, p.M, (int)R, mask,
-                           rowoff, segcnt);
+    if (err == hipSuccess && NGT > 0) {
+        hipLaunchKernelGGL(seg_rows_kernel, dim3((unsigned)((NGT * SU_R + 255) / 256)), dim3(256), 0, s, NGT, NG, p.M,
+                           mask, rowoff, segcnt);
         err = hipGetLastError();
     }
-    if (err == hipSuccess) {   // segment starts: one scan over the (chunk, wave rows) segments
+    if (err == hipSuccess && NGT + 1 <= SEG_SCAN_MAX) {   // segment starts: one scan over the segments
+        hipLaunchKernelGGL(seg_scan_small_kernel, dim3(1), dim3(SEG_SCAN_NT), 0, s, NGT, segcnt, seg);
+        err = hipGetLastError();
+    } else if (err == hipSuccess) {
         const SegPad sp{segcnt, NGT};
         auto seg_it = rocprim::make_transform_iterator(rocprim::counting_iterator<int64_t>(0), sp);
         err = rocprim::exclusive_scan(tmp, scan_bytes, seg_it, seg, 0, (size_t)(NGT + 1), rocprim::plus<int32_t>(), s);
     }
     if (err == hipSuccess && nnz > 0) {
         hipLaunchKernelGGL(place_kernel<double>, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, rows, cols,
-                           vals, p, mask, rowoff, seg, rec, kmul, (int)R);
+                           vals, p, mask, rowoff, segcnt, seg, rec, kmul, (int)R, SdCfg::PAD);
         err = hipGetLastError();
     }
     if (err == hipSuccess) {
