@@ -829,11 +829,13 @@ int data_as_coo(Stager &st, char fmt, int64_t n_rows, int64_t n_cols, int64_t nn
 }
 
 // submat(S) (rs x cs at (ro_s, co_s)) as a strided device matrix: element (r, c) at ptr[r sr + c sc].
-// S.buff when given (its layout); otherwise a ColMajor device fill of the window, as fill_dense.
+// S.buff when given (its layout); otherwise a device fill of the window, as fill_dense, ColMajor or
+// (row_major) RowMajor -- the caller picks the one whose rows of Y the sparse apply reads
+// contiguously. The values are the same either way.
 template <typename T>
 int submat_dense(Stager &st, const rbh_dense_dist *D, const rbh_state *seed, const T *S_buff, char S_layout,
                  int64_t rs, int64_t cs, int64_t ro_s, int64_t co_s, const T **ptr, int64_t *sr, int64_t *sc,
-                 void **ws, hipStream_t s) {
+                 void **ws, hipStream_t s, bool row_major = false) {
     *ws = nullptr;
     if (S_buff) {
         RBH_REQUIRE(S_layout == 'C' || S_layout == 'R');
@@ -858,10 +860,10 @@ int submat_dense(Stager &st, const rbh_dense_dist *D, const rbh_state *seed, con
     int64_t n_rows_, n_cols_;
     if (nat == 'C') { n_rows_ = cs; n_cols_ = rs; g.pr0 = co_s; g.pc0 = ro_s; }
     else { n_rows_ = rs; n_cols_ = cs; g.pr0 = ro_s; g.pc0 = co_s; }
-    if (rs > 0 && cs > 0) RBH_HIP(launch_fill_t<T>(g, n_rows_, n_cols_, nat != 'C', (T *)*ws, s));
+    if (rs > 0 && cs > 0) RBH_HIP(launch_fill_t<T>(g, n_rows_, n_cols_, (nat != 'C') != row_major, (T *)*ws, s));
     *ptr = (const T *)*ws;
-    *sr = 1;
-    *sc = rs;
+    *sr = row_major ? cs : 1;
+    *sc = row_major ? 1 : rs;
     return RBH_OK;
 }
 
@@ -903,8 +905,11 @@ int sksp3(bool left, char layout, char opS, char opA, int64_t M, int64_t N, int6
     const T *Sp = nullptr;
     int64_t sr = 1, sc = 1;
     void *sws = nullptr, *aws = nullptr;
+    // Y(k, j) = op(Ssub)(j, k) (left) or op(Ssub)(k, j) (right): a RowMajor fill makes Y's rows
+    // contiguous when (left, Trans) or (right, NoTrans)
+    const bool s_row_major = left ? opS == 'T' : opS == 'N';
     int rc = submat_dense<T>(st, D, seed, S_buff, S_layout, rows_submat_S, cols_submat_S, ro_s, co_s, &Sp, &sr, &sc,
-                             &sws, s);
+                             &sws, s, s_row_major);
     const int64_t *ar = nullptr, *ac = nullptr;
     const T *av = nullptr;
     if (!rc) rc = data_as_coo<T>(st, A_fmt, A_rows, A_cols, A_nnz, A_p, A_i, A_v, &ar, &ac, &av, &aws, s);

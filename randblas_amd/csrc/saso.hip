@@ -1409,6 +1409,122 @@ static bool dma_eligible(const SparseApply &p, bool &y_k) {
     return p.unit_vals && (p.alpha == 1.0 || p.alpha == -1.0) && (y_k || y_jd) && !dma_off;
 }
 
+// ------------------------------------------------------------------------------------------
+// 8. Row gather, for sparse operators too sparse for the panel kernels: C(i, :) = beta C(i, :) +
+//    sum over row i's entries (k ascending) of (alpha v) * Y(k, :), with Y's rows contiguous
+//    (ysj == 1; sketch_sparse fills submat(S) that way). A panel kernel stages every
+//    (row block, chunk) panel of Y whether or not the block has entries there, i.e.
+//    M N K / SA_ROWS elements; the gather reads nnz N elements (from L2 / Infinity Cache once Y is
+//    resident), so below the density GATHER_DENSITY it reads less and has no barrier at all.
+//    Same per-element order and roundings as the reference's scalar loop (bitwise).
+// ------------------------------------------------------------------------------------------
+constexpr int GA_NT = 256, GA_CPT = 4;   // threads per workgroup, columns per thread (strided)
+constexpr int64_t GATHER_DENSITY = 256;  // gather when nnz * 256 < M * K
+
+template <typename T>
+__global__ void row_keys_kernel(int64_t nnz, const int64_t *rows, const int64_t *cols, const T *vals,
+                                const SparseApply p, uint64_t *keys, T *kv) {
+    const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (e >= nnz) return;
+    const int64_t wr = rows[e] - p.ro, wc = cols[e] - p.co;
+    const bool in = wr >= 0 && wr < p.win_r && wc >= 0 && wc < p.win_c;
+    const uint64_t i = (uint64_t)(p.transposed ? wc : wr);
+    const uint64_t k = (uint64_t)(p.transposed ? wr : wc);
+    keys[e] = in ? (i << 32) | k : ~(uint64_t)0;
+    kv[e] = (T)p.alpha * vals[e];
+}
+
+// rp[i] = first sorted entry of row i (invalid keys sort last; rp[M] = the valid count)
+__global__ void row_ptr_kernel(int64_t nnz, const uint64_t *keys, int64_t M, int32_t *rp) {
+    const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (e > nnz) return;
+    const uint64_t inval = ~(uint64_t)0;
+    const int64_t cur = (e < nnz && keys[e] != inval) ? (int64_t)(keys[e] >> 32) : M;
+    const int64_t prev = (e == 0) ? -1 : ((keys[e - 1] != inval) ? (int64_t)(keys[e - 1] >> 32) : M);
+    for (int64_t r = prev + 1; r <= cur; ++r) rp[r] = (int32_t)e;
+}
+
+template <typename T>
+__global__ __launch_bounds__(GA_NT) void saso_gather_kernel(const SparseApply p, const int32_t *rp,
+                                                            const uint64_t *keys, const T *kv, int64_t ncb) {
+    const int64_t i = blockIdx.x / ncb;
+    const int64_t j0 = (blockIdx.x % ncb) * (GA_NT * GA_CPT) + threadIdx.x;
+    const T *Y = (const T *)p.Y;
+    T *C = (T *)p.C;
+    const T beta = (T)p.beta;
+    T acc[GA_CPT];
+#pragma unroll
+    for (int q = 0; q < GA_CPT; ++q) {
+        const int64_t j = j0 + (int64_t)q * GA_NT;
+        acc[q] = (beta != (T)0 && j < p.N) ? beta * C[i * p.crs + j * p.ccs] : (T)0;
+    }
+    const int32_t e0 = rp[i], e1 = rp[i + 1];
+    for (int32_t e = e0; e < e1; ++e) {
+        const int64_t k = (int64_t)(uint32_t)keys[e];
+        const T av = kv[e];
+        const T *yr = Y + k * p.ysk;
+#pragma unroll
+        for (int q = 0; q < GA_CPT; ++q) {
+            const int64_t j = j0 + (int64_t)q * GA_NT;
+            if (j < p.N) {
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+                const T prod = av * yr[j];
+                acc[q] = acc[q] + prod;
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < GA_CPT; ++q) {
+        const int64_t j = j0 + (int64_t)q * GA_NT;
+        if (j < p.N) C[i * p.crs + j * p.ccs] = acc[q];
+    }
+}
+
+template <typename T>
+static hipError_t run_sparse_gather(const SparseApply &p, const int64_t *rows, const int64_t *cols, const T *vals,
+                                    int64_t nnz, hipStream_t s) {
+    const size_t n = (size_t)(nnz > 0 ? nnz : 1);
+    int end_bit = 33;
+    while (end_bit < 64 && ((uint64_t)1 << (end_bit - 32)) <= (uint64_t)p.M) ++end_bit;
+    size_t tmp_bytes = 0;
+    hipError_t err = rocprim::radix_sort_pairs(nullptr, tmp_bytes, (uint64_t *)nullptr, (uint64_t *)nullptr,
+                                               (T *)nullptr, (T *)nullptr, n, 0, (unsigned)end_bit, s);
+    if (err != hipSuccess) return err;
+    const size_t bytes = 2 * n * sizeof(uint64_t) + 2 * n * sizeof(T) + (size_t)(p.M + 1) * sizeof(int32_t) +
+                         tmp_bytes + 256;
+    char *ws = nullptr;
+    err = ws_alloc((void **)&ws, bytes, s);
+    if (err != hipSuccess) return err;
+    size_t off = 0;
+    auto carve = [&](size_t b) { void *q = ws + off; off += (b + 15) & ~(size_t)15; return q; };
+    uint64_t *k_in = (uint64_t *)carve(n * sizeof(uint64_t));
+    uint64_t *k_out = (uint64_t *)carve(n * sizeof(uint64_t));
+    T *v_in = (T *)carve(n * sizeof(T));
+    T *v_out = (T *)carve(n * sizeof(T));
+    int32_t *rp = (int32_t *)carve((size_t)(p.M + 1) * sizeof(int32_t));
+    void *tmp = carve(tmp_bytes);
+    if (nnz > 0) {
+        hipLaunchKernelGGL(row_keys_kernel<T>, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, rows, cols,
+                           vals, p, k_in, v_in);
+        err = rocprim::radix_sort_pairs(tmp, tmp_bytes, k_in, k_out, v_in, v_out, (size_t)nnz, 0, (unsigned)end_bit, s);
+    }
+    if (err == hipSuccess) {
+        hipLaunchKernelGGL(row_ptr_kernel, dim3((unsigned)((nnz + 1 + 255) / 256)), dim3(256), 0, s, nnz, k_out, p.M, rp);
+        err = hipGetLastError();
+    }
+    if (err == hipSuccess) {
+        timing_begin(s);
+        const int64_t ncb = (p.N + GA_NT * GA_CPT - 1) / (GA_NT * GA_CPT);
+        hipLaunchKernelGGL(saso_gather_kernel<T>, dim3((unsigned)(p.M * ncb)), dim3(GA_NT), 0, s, p, rp, k_out, v_out, ncb);
+        err = hipGetLastError();
+        timing_end(s);
+    }
+    const hipError_t e2 = ws_free(ws, s);
+    return err != hipSuccess ? err : e2;
+}
+
 template <typename T>
 static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, const int64_t *cols, const T *vals,
                                      int64_t nnz, hipStream_t s) {
@@ -1420,6 +1536,13 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
             const hipError_t e = run_sparse_dma(p, nullptr, rows, cols, (const double *)vals, nnz, y_k, s);
             if (e != hipErrorNotSupported) return e;   // NotSupported: too many records, nothing done
         }
+    }
+    {   // row gather (section 8) for very sparse operators over j-contiguous Y
+        static const bool gather_off = [] { const char *e = getenv("RBH_NO_SASO_GATHER"); return e && e[0] == '1'; }();
+        if (!gather_off && p.ysj == 1 && (double)nnz * GATHER_DENSITY < (double)p.M * (double)p.K &&
+            p.K < ((int64_t)1 << 32) &&
+            p.M < ((int64_t)1 << 31) && p.M * ((p.N + GA_NT * GA_CPT - 1) / (GA_NT * GA_CPT)) < ((int64_t)1 << 31))
+            return run_sparse_gather<T>(p, rows, cols, vals, nnz, s);
     }
     hipError_t err;
     const int64_t nchunks = p.K > 0 ? (p.K + SP_KC - 1) / SP_KC : 0;

@@ -73,7 +73,7 @@ def op(M, o):
     return M if o == "N" else M.T
 
 
-def run_case(cuda, side, layout, fmt, opS, opA, dtype, alpha, beta, dims, offs, identity=False):
+def run_case(cuda, side, layout, fmt, opS, opA, dtype, alpha, beta, dims, offs, identity=False, density=0.08):
     eps = np.finfo(dtype).eps
     ro_s, co_s, ro_a, co_a = offs
     if side == "left":   # B (d x n) = op(Ssub) (d x m) op(Asub) (m x n)
@@ -90,7 +90,7 @@ def run_case(cuda, side, layout, fmt, opS, opA, dtype, alpha, beta, dims, offs, 
     else:   # left_spmm's CSR / CSC branch takes the whole matrix only (spmm_dispatch.hh:100-103)
         ro_a = co_a = 0
         AR, AC = saR, saC
-    rows, cols, vals, Adense = random_sparse(AR, AC, 0.08, 7, dtype)
+    rows, cols, vals, Adense = random_sparse(AR, AC, density, 7, dtype)
     A = as_format(fmt, AR, AC, rows, cols, vals, cuda)
     if identity:
         Sfull = np.eye(SR, SC, dtype=dtype)
@@ -157,6 +157,17 @@ def test_ops_and_scales(cuda, side, layout, fmt, opS, opA):
 def test_submatrices(cuda, side, layout, fmt, dtype):
     """submatrix_self / submatrix_other: windows of both the operator and the data matrix."""
     run_case(cuda, side, layout, fmt, "N", "T", dtype, 2.0, -1.0, (41, 19, 260), (3, 5, 7, 2))
+
+
+@pytest.mark.parametrize("side", ["left", "right"])
+@pytest.mark.parametrize("layout", ["C", "R"])
+@pytest.mark.parametrize("fmt", FMTS)
+@pytest.mark.parametrize("opS,opA", [("N", "N"), ("T", "T")])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_very_sparse_data(cuda, side, layout, fmt, opS, opA, dtype):
+    """Density 0.002 (< 1/256): the row gather (saso.hip section 8) over the j-contiguous fill of submat(S)."""
+    offs = (2, 3, 1, 4) if fmt == "COO" else (2, 3, 0, 0)
+    run_case(cuda, side, layout, fmt, opS, opA, dtype, -1.5, 0.25, (45, 31, 3000), offs, density=0.002)
 
 
 @pytest.mark.parametrize("fmt", FMTS)

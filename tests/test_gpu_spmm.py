@@ -37,14 +37,16 @@ def dense_buf(r, c, ld, layout, seed, dtype):
 @pytest.mark.parametrize("layout", ["C", "R"])
 @pytest.mark.parametrize("opA,opB", [("N", "N"), ("T", "N"), ("N", "T"), ("T", "T")])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
-def test_spmm_left(cuda, fmt, layout, opA, opB, dtype):
-    m, n, k = 33, 21, 140
+@pytest.mark.parametrize("density", [0.1, 0.002])
+def test_spmm_left(cuda, fmt, layout, opA, opB, dtype, density):
+    """density 0.002: below 1/256, so a j-contiguous op(B) takes the row gather (saso.hip section 8)."""
+    m, n, k = (33, 21, 140) if density > 0.01 else (33, 21, 3000)
     AR, AC = (m, k) if opA == "N" else (k, m)
     ro, co = (0, 0)
     if fmt == "COO":   # a window of a larger COO matrix
         ro, co = 3, 5
         AR, AC = AR + 7, AC + 9
-    rows, cols, vals, _ = random_sparse(AR, AC, 0.1, 11, dtype)
+    rows, cols, vals, _ = random_sparse(AR, AC, density, 11, dtype)
     A = as_format(fmt, AR, AC, rows, cols, vals, cuda)
     rB, cB = (k, n) if opB == "N" else (n, k)
     ldb = (rB if layout == "C" else cB) + 2
