@@ -648,6 +648,24 @@ template <> struct SuAcc<double> {
                      : "m0", "scc");
     }
 };
+#ifndef SU_F32_NOP
+#define SU_F32_NOP 0
+#endif
+#if SU_F32_NOP == 1
+#define SU_F32_NOP_A "s_nop 4\n\t"
+#else
+#define SU_F32_NOP_A ""
+#endif
+#if SU_F32_NOP == 2
+#define SU_F32_NOP_B "s_nop 4\n\t"
+#else
+#define SU_F32_NOP_B ""
+#endif
+#if SU_F32_NOP == 3
+#define SU_F32_NOP_C "s_nop 0\n\t"
+#else
+#define SU_F32_NOP_C ""
+#endif
 template <> struct SuAcc<float> {
     typedef float v32 __attribute__((ext_vector_type(32)));
     v32 a;
@@ -660,8 +678,11 @@ template <> struct SuAcc<float> {
         float t;
         asm volatile("v_xor_b32 %1, %3, %4\n\t"
                      "s_waitcnt lgkmcnt(0)\n\t"
+                     SU_F32_NOP_A
                      "s_set_gpr_idx_on %2, gpr_idx(SRC0,DST)\n\t"
+                     SU_F32_NOP_C
                      "v_add_f32 v32, v32, %1\n\t"
+                     SU_F32_NOP_B
                      "s_set_gpr_idx_off"
                      : "+{v[32:63]}"(a), "=&v"(t)
                      : "s"(__builtin_amdgcn_readfirstlane(rec)), "s"(__builtin_amdgcn_readfirstlane(rec & 0x80000000u)),

@@ -809,6 +809,201 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// f32 wide tile with 32-deep K steps: 64 generated x 512 memory outer indices
+// ------------------------------------------------------------------------------------------
+// The f32 form of skge_wide_kernel. A K step is 32 deep, so each memory row contributes one whole
+// 128-B line per step: with 16-deep steps every line was fetched in two halves one step apart,
+// and lines 128 KiB apart (C4's column stride) were evicted from L2 in between (PMC: 18.8 GB read
+// per launch for |A| = 4.29 GB). It also halves the barriers per unit of MFMA work.
+// * Memory tile: 512 rows x 32 floats (64 KB per stage), unpadded 128-B rows with 16-B slot v of
+//   row o at v ^ (o & 7). Thread tid stages vectors tid + 512 e (e < 8): row (tid >> 3) + 64 e,
+//   slot tid & 7, through 4-vector register halves (the second loaded mid-step).
+// * Generated tile: 64 x 32 (512 Philox calls per step, one per thread: every wave draws), the same
+//   swizzled 128-B rows.
+// * 8 waves along the memory dimension, each 64 x 64 = 4 x 4 v_mfma_f32_16x16x4f32 tiles (64
+//   accumulator VGPRs). Lane (g, r) reads 16 B (k = 8g + 4h .. + 3) of a fragment row per half h;
+//   sub-step (h, s) contracts k = 8g + 4h + s in both operands.
+// Requires K % 32 == 0, a mode-2 memory operand, pc0 % 4 == 0 and 512 rows of the memory operand
+// addressable with 32-bit byte offsets.
+constexpr int KB32 = 32;
+
+template <int GK, int FAMILY, bool GX, bool SPLIT>
+__global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
+    typedef float T;
+    constexpr int BG = 64, BMM = 512, WMW = 8;
+    constexpr int FA = BG / 16, FB = BMM / 16 / WMW;
+    constexpr int MS = BMM * KB32, GS = BG * KB32;   // floats per stage
+    typedef Mfma<T>::v4 acc_t;
+    typedef float v4f __attribute__((ext_vector_type(4)));
+
+    __shared__ __attribute__((aligned(16))) T lds[2 * MS + 2 * GS];   // [mem 0 | mem 1 | gen 0 | gen 1]
+    __shared__ rb::LogfEntry tab[16];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, r = lane & 15;
+    if (tid < 16) tab[tid] = rb::LOGF_TAB[tid];
+
+    const GenOperand &gop = GX ? p.xg : p.yg;
+    const MemOperand &mop = GX ? p.ym : p.xm;
+    const int64_t gnO = GX ? p.M : p.N, mnO = GX ? p.N : p.M;
+    const int64_t nTg = (gnO + BG - 1) / BG, nTm = (mnO + BMM - 1) / BMM;
+    const int split = SPLIT ? p.splitk : 1;
+    const int64_t nb = nTg * nTm * split;
+    const int64_t b = blockIdx.x;
+    const int64_t xcd = b % 8, qq = nb / 8, rr = nb % 8;
+    const int64_t t_all = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + b / 8;
+    const int64_t z = t_all % split, t = t_all / split;
+    const int64_t go0 = (t % nTg) * BG, mo0 = (t / nTg) * BMM;
+
+    const T *mptr = (const T *)mop.ptr;
+    v4f rs[4];
+    const char *mtile = (const char *)(mptr + mo0 * mop.so);
+    const uint32_t vstep = (uint32_t)(64 * mop.so * (int64_t)sizeof(T));
+    const uint32_t voff0 = (uint32_t)(((tid >> 3) * mop.so + 4 * (tid & 7)) * (int64_t)sizeof(T));
+    const uint32_t vmax = (uint32_t)(((mnO - 1 - mo0) * mop.so + 4 * (tid & 7)) * (int64_t)sizeof(T));
+    const int lwoff = (tid >> 3) * KB32 + 4 * ((tid & 7) ^ ((tid >> 3) & 7));   // floats, + 64 * KB32 * e
+    auto rload = [&](int64_t k0, int half) {
+        const int64_t ck0 = k0 < p.K ? k0 : p.K - KB32;
+        const char *base = mtile + ck0 * (int64_t)sizeof(T);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const uint32_t vo = voff0 + (uint32_t)(4 * half + e) * vstep;
+            rs[e] = *reinterpret_cast<const v4f *>(base + (vo < vmax ? vo : vmax));
+        }
+    };
+    auto rstore = [&](int st, int half) {
+        T *dst = lds + st * MS + lwoff;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) *reinterpret_cast<v4f *>(dst + 64 * KB32 * (4 * half + e)) = rs[e];
+    };
+
+    // one Philox call per thread: GEN_OK row tid >> 3, k quad tid & 7; GEN_OO k = tid >> 4, outer quad tid & 15
+    T gv[4];
+    const bool glane_ok = GK == GEN_OK ? go0 + (tid >> 3) < gnO : true;
+    const bool gtile_full = go0 + BG <= gnO;
+    auto draw = [&](int64_t kt) {
+        uint32_t c[4];
+        {
+            uint64_t off;
+            if (GK == GEN_OK) {
+                const int o = tid >> 3, q = tid & 7;
+                off = (uint64_t)(gop.pr0 + go0 + o) * gop.stride + (uint64_t)(gop.pc0 >> 2) + q + (uint64_t)kt * (KB32 / 4);
+            } else {
+                const int k = tid >> 4, q = tid & 15;
+                off = (uint64_t)(gop.pr0 + kt * KB32 + k) * gop.stride + (uint64_t)((gop.pc0 + go0) >> 2) + q;
+            }
+            rb::ctr_add(gop.ctr, off, c);
+        }
+        const rb::u32x4 w = rb::philox4x32<10>(c[0], c[1], c[2], c[3], gop.key[0], gop.key[1]);
+        float sm[4];
+        rb::sample4<FAMILY>(w, sm, tab);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) gv[e] = FAMILY == rb::UNIFORM ? sm[e] * (T)gop.scale : sm[e];
+        if (!gtile_full || kt * KB32 >= p.K) {   // uniform: edge tile or the prefetch past K
+            if (GK == GEN_OK) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) gv[e] = (glane_ok && kt * KB32 < p.K) ? gv[e] : (T)0;
+            } else {
+                const int q = tid & 15;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) gv[e] = (go0 + 4 * q + e < gnO && kt * KB32 < p.K) ? gv[e] : (T)0;
+            }
+        }
+    };
+    auto gstore = [&](int st) {
+        T *G = lds + 2 * MS + st * GS;
+        if (GK == GEN_OK) {
+            const int o = tid >> 3, q = tid & 7;
+            v4f x;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[e] = gv[e];
+            *reinterpret_cast<v4f *>(G + o * KB32 + 4 * (q ^ (o & 7))) = x;
+        } else {
+            const int k = tid >> 4, q = tid & 15;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int o = 4 * q + e;
+                G[o * KB32 + 4 * ((k >> 2) ^ (o & 7)) + (k & 3)] = gv[e];
+            }
+        }
+    };
+
+    acc_t acc[FA][FB];
+#pragma unroll
+    for (int a = 0; a < FA; ++a)
+#pragma unroll
+        for (int c = 0; c < FB; ++c) acc[a][c] = (acc_t){0, 0, 0, 0};
+
+    const int64_t nk = p.K / KB32;
+    const int64_t per = SPLIT ? (nk + split - 1) / split : nk;
+    const int64_t kt0 = SPLIT ? z * per : 0, kt1 = SPLIT ? (kt0 + per < nk ? kt0 + per : nk) : nk;
+    __syncthreads();   // tab
+    rload(kt0 * KB32, 0); rstore(0, 0); rload(kt0 * KB32, 1); rstore(0, 1);
+    draw(kt0); gstore(0);
+    __syncthreads();
+
+    // fragment rows (floats, relative to the stage base); the swizzle of rows 16 a + r is r & 7
+    const int grow = r * KB32;                    // + 16 * a * KB32
+    const int mrow = (16 * FB * wave + r) * KB32;  // + 16 * c * KB32
+    const int sw = r & 7;
+    auto k_loop = [&]() {
+    for (int64_t kt = kt0; kt < kt1; ++kt) {
+        const int cur = (int)((kt - kt0) & 1);
+        const T *Mc = lds + cur * MS;
+        const T *Gc = lds + 2 * MS + cur * GS;
+        const int64_t kn = (kt + 1) * KB32;
+        rload(kn, 0);
+        draw(kt + 1);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (h == 1) { rstore(cur ^ 1, 0); rload(kn, 1); }
+            const int slot = 4 * ((2 * g + h) ^ sw);
+            v4f gf[FA], mf[FB];
+#pragma unroll
+            for (int a = 0; a < FA; ++a) gf[a] = *reinterpret_cast<const v4f *>(Gc + grow + 16 * a * KB32 + slot);
+#pragma unroll
+            for (int c = 0; c < FB; ++c) mf[c] = *reinterpret_cast<const v4f *>(Mc + mrow + 16 * c * KB32 + slot);
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int a = 0; a < FA; ++a)
+#pragma unroll
+                    for (int c = 0; c < FB; ++c)
+                        acc[a][c] = GX ? Mfma<T>::mma(mf[c][s], gf[a][s], acc[a][c])
+                                       : Mfma<T>::mma(gf[a][s], mf[c][s], acc[a][c]);
+        }
+        gstore(cur ^ 1);
+        rstore(cur ^ 1, 1);
+        __syncthreads();
+    }
+    };
+    k_loop();
+
+    T *C = SPLIT ? (T *)p.partial + z * p.M * p.N : (T *)p.C;
+    const int64_t ldc = SPLIT ? p.M : p.ldc;
+    const T alpha = (T)p.alpha, beta = SPLIT ? (T)0 : (T)p.beta;
+#pragma unroll
+    for (int a = 0; a < FA; ++a)
+#pragma unroll
+    for (int c = 0; c < FB; ++c) {
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+            const int dr = Mfma<T>::drow(lane, reg);
+            const int64_t gi = go0 + 16 * a, mi = mo0 + 16 * FB * wave + 16 * c;
+            const int64_t i = GX ? gi + r : mi + r;
+            const int64_t j = GX ? mi + dr : gi + dr;
+            if (i < p.M && j < p.N) {
+                T *dst = C + i + j * ldc;
+                const T v = alpha * acc[a][c][reg];
+                *dst = (beta == (T)0) ? v : v + beta * *dst;
+            }
+        }
+    }
+}
+
 // split-K: C = sum_z partial[z] + beta C (partials already carry alpha), in a fixed order
 template <typename T>
 __global__ void splitk_reduce_kernel(int64_t M, int64_t N, int split, const T *partial, T beta, T *C, int64_t ldc) {
@@ -947,10 +1142,57 @@ static hipError_t launch_wide(const GemmProblem &p, hipStream_t s) {
     return e;
 }
 
+// the wide kernels address 512 rows of the memory operand with 32-bit byte offsets
+template <typename T>
+static bool wide_offsets_ok(const GemmProblem &p) {
+    const MemOperand &m = p.xkind == MEM ? p.xm : p.ym;
+    return (int64_t)512 * m.so * (int64_t)sizeof(T) < ((int64_t)1 << 32);
+}
+
 template <typename T>
 static bool wide_ok(const GemmProblem &p) {
     static const bool off = [] { const char *e = getenv("RBH_NO_WIDE"); return e && e[0] == '1'; }();
-    return sizeof(T) == 8 && !off && fused_ok(p) && p.K % BK == 0;
+    return sizeof(T) == 8 && !off && fused_ok(p) && p.K % BK == 0 && wide_offsets_ok<T>(p);
+}
+
+template <int GK, int FAMILY, bool GX>
+static hipError_t launch_wide32(const GemmProblem &p, hipStream_t s) {
+    typedef float T;
+    const int64_t gnO = GX ? p.M : p.N, mnO = GX ? p.N : p.M;
+    const int64_t nb = ((gnO + 63) / 64) * ((mnO + 511) / 512);
+    if (nb <= 0) return hipSuccess;
+    // split-K on the same terms as the 16-deep kernels (the split counts 16-deep steps)
+    const int split = choose_split(nb, p.K / BK);
+    GemmProblem q = p;
+    q.splitk = split;
+    q.partial = nullptr;
+    hipError_t e;
+    if (split > 1) {
+        e = ws_alloc(&q.partial, sizeof(T) * (size_t)split * p.M * p.N, s);
+        if (e != hipSuccess) return e;
+    }
+    timing_begin(s);
+    if (split > 1) hipLaunchKernelGGL((skge_wide32_kernel<GK, FAMILY, GX, true>), dim3((unsigned)(nb * split)), dim3(512), 0, s, q);
+    else hipLaunchKernelGGL((skge_wide32_kernel<GK, FAMILY, GX, false>), dim3((unsigned)nb), dim3(512), 0, s, q);
+    e = hipGetLastError();
+    if (split > 1 && e == hipSuccess) {
+        hipLaunchKernelGGL(splitk_reduce_kernel<T>, dim3(2048), dim3(256), 0, s, p.M, p.N, split,
+                           (const T *)q.partial, (T)p.beta, (T *)p.C, p.ldc);
+        e = hipGetLastError();
+    }
+    timing_end(s);
+    if (split > 1) {
+        const hipError_t e2 = ws_free(q.partial, s);
+        if (e == hipSuccess) e = e2;
+    }
+    return e;
+}
+
+// f32 on the 32-deep wide kernel: K % 32 == 0 (RBH_NO_WIDE32=1 keeps the 16-deep fused kernel)
+template <typename T>
+static bool wide32_ok(const GemmProblem &p) {
+    static const bool off = [] { const char *e = getenv("RBH_NO_WIDE32"); return e && e[0] == '1'; }();
+    return sizeof(T) == 4 && !off && fused_ok(p) && p.K % KB32 == 0 && wide_offsets_ok<T>(p);
 }
 
 // One-triangle symmetric memory operand: the wide f64 kernel when the generated operand runs its
@@ -996,6 +1238,15 @@ static hipError_t launch_gemm(const GemmProblem &p, hipStream_t s) {
         if (p.ykind == GEN_OK) { RBH_WIDE_L(GEN_OK, false); }
         if (p.ykind == GEN_OO) { RBH_WIDE_L(GEN_OO, false); }
 #undef RBH_WIDE_L
+    }
+    if (wide32_ok<T>(p)) {
+#define RBH_WIDE32_L(GK, GX)                                                                   \
+    return unif ? launch_wide32<GK, rb::UNIFORM, GX>(p, s) : launch_wide32<GK, rb::GAUSSIAN, GX>(p, s)
+        if (p.xkind == GEN_OK) { RBH_WIDE32_L(GEN_OK, true); }
+        if (p.xkind == GEN_OO) { RBH_WIDE32_L(GEN_OO, true); }
+        if (p.ykind == GEN_OK) { RBH_WIDE32_L(GEN_OK, false); }
+        if (p.ykind == GEN_OO) { RBH_WIDE32_L(GEN_OO, false); }
+#undef RBH_WIDE32_L
     }
     if (fused_ok(p)) {
         // tile (generated x memory outer indices) and waves; f32 variants selectable for tuning

@@ -87,9 +87,14 @@ if os.environ.get("DBG_F64_UNIT") == "1":   # f64 user arrays with +-1 values: t
             for f in ("unit", "scaled"):
                 run(f, np.float64, lay, d=1000, n=130, m=2048, vec=8, key=7, sampled=False)
     sys.exit(0)
-if os.environ.get("DBG_SAMPLED") == "1":
-    for rep in range(3):
-        for dt in (np.float32, np.float64):
+if os.environ.get("DBG_F32_USER") == "1":   # f32 user arrays with +-1 values (unit kernel under RBH_SASO_F32_UNIT=1)
+    for rep in range(int(os.environ.get("DBG_REPS", "3"))):
+        for lay in ("C", "R"):
+            run("unit", np.float32, lay, d=1000, n=130, m=2048, vec=8, key=7, sampled=False)
+    sys.exit(0)
+if os.environ.get("DBG_SAMPLED") == "1":   # sampled operators; DBG_F32_ONLY=1 skips f64
+    for rep in range(int(os.environ.get("DBG_REPS", "3"))):
+        for dt in (np.float32,) if os.environ.get("DBG_F32_ONLY") == "1" else (np.float32, np.float64):
             for lay in ("C", "R"):
                 run("unit", dt, lay, d=1000, n=130, m=2048, vec=8, key=7, sampled=True)
     sys.exit(0)
