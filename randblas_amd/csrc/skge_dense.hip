@@ -817,8 +817,11 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
 // and lines 128 KiB apart (C4's column stride) were evicted from L2 in between (PMC: 18.8 GB read
 // per launch for |A| = 4.29 GB). It also halves the barriers per unit of MFMA work.
 // * Memory tile: 512 rows x 32 floats (64 KB per stage), unpadded 128-B rows with 16-B slot v of
-//   row o at v ^ (o & 7). Thread tid stages vectors tid + 512 e (e < 8): row (tid >> 3) + 64 e,
-//   slot tid & 7, through 4-vector register halves (the second loaded mid-step).
+//   row o at v ^ sw32(o): every 16-lane group of a ds_read_b128 fragment read (lanes {0-3, 12-15,
+//   20-27} etc., MI355X_MICROARCH.md LDS table) then covers all 64 banks, and a row's 8 slots stay
+//   distinct for the 8-lane groups of the ds_write_b128 staging. Thread tid stages vectors
+//   tid + 512 e (e < 8): row (tid >> 3) + 64 e, slot tid & 7, through 4-vector register halves
+//   (the second loaded mid-step).
 // * Generated tile: 64 x 32 (512 Philox calls per step, one per thread: every wave draws), the same
 //   swizzled 128-B rows.
 // * 8 waves along the memory dimension, each 64 x 64 = 4 x 4 v_mfma_f32_16x16x4f32 tiles (64
@@ -827,6 +830,9 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
 // Requires K % 32 == 0, a mode-2 memory operand, pc0 % 4 == 0 and 512 rows of the memory operand
 // addressable with 32-bit byte offsets.
 constexpr int KB32 = 32;
+// slot swizzle of row o: bit 1 of o -> bit 0, bit 3 -> bit 2 (lanes r and r + 4 / r + 8 of a read
+// group land in different bank quads)
+__device__ __forceinline__ int sw32(int o) { return ((o >> 1) & 1) | ((o >> 1) & 4); }
 
 template <int GK, int FAMILY, bool GX, bool SPLIT>
 __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
@@ -864,7 +870,7 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
     const uint32_t vstep = (uint32_t)(64 * mop.so * (int64_t)sizeof(T));
     const uint32_t voff0 = (uint32_t)(((tid >> 3) * mop.so + 4 * (tid & 7)) * (int64_t)sizeof(T));
     const uint32_t vmax = (uint32_t)(((mnO - 1 - mo0) * mop.so + 4 * (tid & 7)) * (int64_t)sizeof(T));
-    const int lwoff = (tid >> 3) * KB32 + 4 * ((tid & 7) ^ ((tid >> 3) & 7));   // floats, + 64 * KB32 * e
+    const int lwoff = (tid >> 3) * KB32 + 4 * ((tid & 7) ^ sw32(tid >> 3));   // floats, + 64 * KB32 * e
     auto rload = [&](int64_t k0, int half) {
         const int64_t ck0 = k0 < p.K ? k0 : p.K - KB32;
         const char *base = mtile + ck0 * (int64_t)sizeof(T);
@@ -920,13 +926,13 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
             v4f x;
 #pragma unroll
             for (int e = 0; e < 4; ++e) x[e] = gv[e];
-            *reinterpret_cast<v4f *>(G + o * KB32 + 4 * (q ^ (o & 7))) = x;
+            *reinterpret_cast<v4f *>(G + o * KB32 + 4 * (q ^ sw32(o))) = x;
         } else {
             const int k = tid >> 4, q = tid & 15;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int o = 4 * q + e;
-                G[o * KB32 + 4 * ((k >> 2) ^ (o & 7)) + (k & 3)] = gv[e];
+                G[o * KB32 + 4 * ((k >> 2) ^ sw32(o)) + (k & 3)] = gv[e];
             }
         }
     };
@@ -945,18 +951,21 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
     draw(kt0); gstore(0);
     __syncthreads();
 
-    // fragment rows (floats, relative to the stage base); the swizzle of rows 16 a + r is r & 7
+    // fragment rows (floats, relative to the stage base); the swizzle of rows 16 a + r is sw32(r)
     const int grow = r * KB32;                    // + 16 * a * KB32
     const int mrow = (16 * FB * wave + r) * KB32;  // + 16 * c * KB32
-    const int sw = r & 7;
-    auto k_loop = [&]() {
+    const int sw = sw32(r);
+    // Waves w and w + 4 share a SIMD and take the step's draw and MFMAs in opposite order, so one
+    // feeds the matrix pipe while the other draws (two copies of the loop, one order each).
+    auto k_loop = [&](auto mfma_first_tag) {
+    constexpr bool MFMA_FIRST = decltype(mfma_first_tag)::value;
     for (int64_t kt = kt0; kt < kt1; ++kt) {
         const int cur = (int)((kt - kt0) & 1);
         const T *Mc = lds + cur * MS;
         const T *Gc = lds + 2 * MS + cur * GS;
         const int64_t kn = (kt + 1) * KB32;
         rload(kn, 0);
-        draw(kt + 1);
+        if (!MFMA_FIRST) draw(kt + 1);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             if (h == 1) { rstore(cur ^ 1, 0); rload(kn, 1); }
@@ -975,12 +984,17 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
                         acc[a][c] = GX ? Mfma<T>::mma(mf[c][s], gf[a][s], acc[a][c])
                                        : Mfma<T>::mma(gf[a][s], mf[c][s], acc[a][c]);
         }
+        if (MFMA_FIRST) draw(kt + 1);
         gstore(cur ^ 1);
         rstore(cur ^ 1, 1);
         __syncthreads();
     }
     };
-    k_loop();
+#ifndef RBH_W32_PHASE
+#define RBH_W32_PHASE 1
+#endif
+    if (!RBH_W32_PHASE || ((wave >> 2) & 1) == 0) k_loop(std::true_type{});
+    else k_loop(std::false_type{});
 
     T *C = SPLIT ? (T *)p.partial + z * p.M * p.N : (T *)p.C;
     const int64_t ldc = SPLIT ? p.M : p.ldc;
