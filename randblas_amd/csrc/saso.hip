@@ -626,6 +626,14 @@ __device__ __forceinline__ void su_panel_store(const T (&st)[SuCfg<T>::NST], uin
 
 // The accumulators: 32 rows per lane in two pinned register blocks, v[32:63] and v[64:95] for f64
 // (v[32:63] for f32), so that GPR index mode can address row i's accumulator as v32 + idx.
+// Wait state: s_set_gpr_idx_on / s_set_gpr_idx_idx write the index into M0, and the indexed VALU
+// instruction reads M0 when it issues. Like the SALU M0 write -> v_movrel* pair of the GFX9 wait-state
+// table (LLVM's hasReadM0MovRelInterpHazard), it needs one wait state in between, which no
+// compiler pass inserts inside an asm string. Without it the VALU took the previous section's
+// index: an entry was added into the row of the entry before it (or, on a wave's first section,
+// into whatever register M0 pointed at -- the illegal-address faults). The round-2 f32 stress
+// (tools/f32_sampled_stress.sh, d = 1000, m = 2048, n = 130) failed 39 of 60 runs without the
+// s_nop 0 and with one placed before s_set_gpr_idx_on instead, and passed 60 of 60 with it.
 template <typename T> struct SuAcc;
 template <> struct SuAcc<double> {
     typedef double v16 __attribute__((ext_vector_type(16)));
@@ -641,6 +649,7 @@ template <> struct SuAcc<double> {
         if (SU_ABL & 8) { a[0] += ys; return; }   // diagnostics: static row
         asm volatile("s_waitcnt lgkmcnt(0)\n\t"
                      "s_set_gpr_idx_on %2, gpr_idx(SRC0,DST)\n\t"
+                     "s_nop 0\n\t"   // M0 -> indexed VALU wait state (see below)
                      "v_add_f64 v[32:33], v[32:33], %3\n\t"
                      "s_set_gpr_idx_off"
                      : "+{v[32:63]}"(a), "+{v[64:95]}"(b)
@@ -648,41 +657,20 @@ template <> struct SuAcc<double> {
                      : "m0", "scc");
     }
 };
-#ifndef SU_F32_NOP
-#define SU_F32_NOP 0
-#endif
-#if SU_F32_NOP == 1
-#define SU_F32_NOP_A "s_nop 4\n\t"
-#else
-#define SU_F32_NOP_A ""
-#endif
-#if SU_F32_NOP == 2
-#define SU_F32_NOP_B "s_nop 4\n\t"
-#else
-#define SU_F32_NOP_B ""
-#endif
-#if SU_F32_NOP == 3
-#define SU_F32_NOP_C "s_nop 0\n\t"
-#else
-#define SU_F32_NOP_C ""
-#endif
 template <> struct SuAcc<float> {
     typedef float v32 __attribute__((ext_vector_type(32)));
     v32 a;
     __device__ __forceinline__ float get(int r) const { return a[r]; }
     __device__ __forceinline__ void set(int r, float x) { a[r] = x; }
-    // The sign flip is inside the asm, from a scalar mask (a compiler-fused v_bitop3_b32 reading
-    // the record's SGPR right before s_set_gpr_idx_on lost whole entries).
+    // The sign flip is inside the asm, from a scalar mask.
     __device__ __forceinline__ void add_at(uint32_t rec, float y) {
         if (SU_ABL & 8) { a[0] += __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, y) ^ (rec & 0x80000000u)); return; }
         float t;
         asm volatile("v_xor_b32 %1, %3, %4\n\t"
                      "s_waitcnt lgkmcnt(0)\n\t"
-                     SU_F32_NOP_A
                      "s_set_gpr_idx_on %2, gpr_idx(SRC0,DST)\n\t"
-                     SU_F32_NOP_C
+                     "s_nop 0\n\t"   // M0 -> indexed VALU wait state
                      "v_add_f32 v32, v32, %1\n\t"
-                     SU_F32_NOP_B
                      "s_set_gpr_idx_off"
                      : "+{v[32:63]}"(a), "=&v"(t)
                      : "s"(__builtin_amdgcn_readfirstlane(rec)), "s"(__builtin_amdgcn_readfirstlane(rec & 0x80000000u)),
@@ -925,10 +913,9 @@ struct SdAcc {
 };
 
 // Four entries in one index-mode section: the row index moves with s_set_gpr_idx_idx, so the mode
-// is toggled once per four adds (the sign flips are done before the section). LDS reads of the
-// walk stay in flight across the section. Index mode relocates the VGPR operands of VALU
-// instructions; LLVM's own index-mode code (SIInsertWaitcnts has no drain rule for
-// s_set_gpr_idx_on) keeps memory returns in flight across it the same way.
+// is toggled once per four adds (the sign flips are done before the section), each index write
+// followed by its M0 wait state (section 4). LDS reads of the walk stay in flight across the
+// section: index mode relocates the VGPR operands of VALU instructions, not memory returns.
 __device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t *w, const double *y) {
     double ys[4];
 #pragma unroll
@@ -938,12 +925,16 @@ __device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t *w, const dou
         ys[q] = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, y[q]) ^ ((uint64_t)m << 32));
     }
     asm volatile("s_set_gpr_idx_on %3, gpr_idx(SRC0,DST)\n\t"
+                 "s_nop 0\n\t"
                  "v_add_f64 v[32:33], v[32:33], %7\n\t"
                  "s_set_gpr_idx_idx %4\n\t"
+                 "s_nop 0\n\t"
                  "v_add_f64 v[32:33], v[32:33], %8\n\t"
                  "s_set_gpr_idx_idx %5\n\t"
+                 "s_nop 0\n\t"
                  "v_add_f64 v[32:33], v[32:33], %9\n\t"
                  "s_set_gpr_idx_idx %6\n\t"
+                 "s_nop 0\n\t"
                  "v_add_f64 v[32:33], v[32:33], %10\n\t"
                  "s_set_gpr_idx_off"
                  : "+{v[32:63]}"(acc.a), "+{v[64:95]}"(acc.b), "+{v[96:97]}"(acc.dmy)
@@ -1605,13 +1596,7 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
     const bool y_j = p.ysj == 1;
     const bool y_k = p.ysk == 1 && (p.ysj % VEC) == 0 && (((uintptr_t)p.Y) % 16) == 0 && (p.K % VEC) == 0;
     static const bool unit_off = [] { const char *e = getenv("RBH_NO_SASO_UNIT"); return e && e[0] == '1'; }();
-    // f64 only. The f32 instantiation loses whole panel rows on gfx950 (round-2 stress,
-    // tools/f32_stress.sh: sampled f32, RowMajor, d=1000, m=2048, n=130: k = 124 or 60 mod 128 --
-    // the staging registers of one wave -- missing from one 64-column block, and once an illegal
-    // address), while the f64 one at the same shape ran 160 of 160 clean; f32 takes the
-    // general-value kernel (RBH_SASO_F32_UNIT=1 routes it here for that stress)
-    static const bool f32_unit = [] { const char *e = getenv("RBH_SASO_F32_UNIT"); return e && e[0] == '1'; }();
-    const bool unit = (y_j || y_k) && !unit_off && (sizeof(T) == 8 || f32_unit);
+    const bool unit = (y_j || y_k) && !unit_off;
 
     err = hipMemsetAsync(ut, 0, sizeof(UniformTest<T>), s);
     if (err != hipSuccess) { (void)ws_free(ws, s); return err; }

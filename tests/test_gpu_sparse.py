@@ -188,3 +188,31 @@ def test_lskges_alpha_zero(cuda):
     S = rb.SparseSkOp(rb.SparseDist(19, 201, 3), rb.RNGState(0))
     rb.sketch_general_left("C", "N", "N", 19, 12, 201, 0.0, S, dev(np.ones(201 * 12), cuda), 201, -1.0, dB, 19)
     assert np.array_equal(host(dB), -B0)
+
+
+# Repeated runs of the uniform-value (GPR index mode) kernels at the shape whose f32 runs lost or
+# misplaced entries before the M0 wait state after s_set_gpr_idx_on/_idx (saso.hip section 4):
+# 39 of 60 runs failed then. Every repetition must be bitwise.
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("layout", ["C", "R"])
+@pytest.mark.parametrize("given", [False, True])
+def test_index_mode_repeated(cuda, dtype, layout, given):
+    d, n, m, vec, key = 1000, 130, 2048, 8, 7
+    A = O.random_matrix(m, n, 99, dtype)
+    lda = m if layout == "C" else n
+    ldb = d if layout == "C" else n
+    rows, cols, vals = O.fill_sparse(d, m, vec, "S", key=key, dtype=dtype)
+    Bexp = np.zeros(d * n, dtype=dtype)
+    O.left_spmm_coo(layout, "N", "N", d, n, m, 1.0, d, m, rows, cols, vals, 0, 0, A, lda, 0.0, Bexp, ldb)
+    dA = dev(A, cuda)
+    perm = np.random.default_rng(5).permutation(len(rows))
+    for rep in range(10):
+        S = rb.SparseSkOp(rb.SparseDist(d, m, vec, "S"), rb.RNGState(key=key))
+        if given:
+            S.rows, S.cols, S.vals = dev(rows[perm], cuda), dev(cols[perm], cuda), dev(vals[perm], cuda)
+            S.nnz = len(rows)
+        dB = torch.full((d * n,), float("nan"), dtype=torch.float64 if dtype == np.float64 else torch.float32,
+                        device=cuda)
+        rb.sketch_general_left(layout, "N", "N", d, n, m, 1.0, S, dA, lda, 0.0, dB, ldb)
+        got = host(dB)
+        assert np.array_equal(bits(got), bits(Bexp)), f"repetition {rep}: {np.count_nonzero(bits(got) != bits(Bexp))} differ"

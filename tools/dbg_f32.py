@@ -87,7 +87,7 @@ if os.environ.get("DBG_F64_UNIT") == "1":   # f64 user arrays with +-1 values: t
             for f in ("unit", "scaled"):
                 run(f, np.float64, lay, d=1000, n=130, m=2048, vec=8, key=7, sampled=False)
     sys.exit(0)
-if os.environ.get("DBG_F32_USER") == "1":   # f32 user arrays with +-1 values (unit kernel under RBH_SASO_F32_UNIT=1)
+if os.environ.get("DBG_F32_USER") == "1":   # f32 user arrays with +-1 values (unit kernel)
     for rep in range(int(os.environ.get("DBG_REPS", "3"))):
         for lay in ("C", "R"):
             run("unit", np.float32, lay, d=1000, n=130, m=2048, vec=8, key=7, sampled=False)
