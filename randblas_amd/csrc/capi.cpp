@@ -56,108 +56,83 @@ void timing_end(hipStream_t s) {
     g_timing.used++;
 }
 
-// Workspaces: one stream-ordered pool per device, created on first use and private to this
-// library (the client's default pool is never touched). The pool never returns memory to the
-// system (release threshold = max): with a threshold of 0 it trims at every synchronisation, and a
-// block allocated after such a trim was observed to lose a kernel's writes in a C++ client that
-// also stages host arrays through hipMalloc (B read back as zeros; memset of the fresh block then
-// faulted). DESIGN.md §7 records the study; RBH_POOL_KEEP_BYTES overrides the threshold for it.
+// Workspaces: one arena per (device, stream), backed by hipMalloc blocks that the arena keeps.
+// A call carves its workspaces from the stream's current block (bump allocation) and frees
+// nothing to the runtime: reuse within one stream needs no wait, because the stream orders the
+// work. (hipFreeAsync blocked the host for about as long as the stream's queued work -- 0.44 ms
+// per C3 call -- so a call that freed to the runtime kept the host from running ahead of the GPU.)
+// A request that does not fit opens a larger block; the old one is retired and released (hipFree,
+// which synchronises the device first) once none of its workspaces is live, so growth costs a
+// synchronisation only the few times the arena grows.
 //
-// On top of the pool, one arena per (device, stream): workspaces are carved from a block the
-// stream keeps, so a call frees nothing back to the pool. hipFreeAsync blocks the host for about as
-// long as the stream's queued work (measured 0.44 ms per C3 call), which kept the host from running
-// ahead of the GPU; reuse within one stream is safe without it, because the stream orders the work.
-// A request that does not fit grows the arena when it is empty, else takes a plain pool block.
+// Why not HIP's stream-ordered memory pools: on this ROCm an allocation that reuses a block
+// freed with hipFreeAsync on the same stream occasionally loses a kernel's writes (a whole block
+// read back wrong in 1 of 100-300 iterations; no library code involved: tools/micro/pool_live.hip,
+// hipMalloc control clean). That was the "B read back as zeros" of the C++ client when the pool
+// trimmed at every synchronisation.
 namespace {
-std::mutex g_pool_mu;
-hipMemPool_t g_pool[64] = {};
+std::mutex g_ws_mu;
 struct Arena {
-    char *base = nullptr;
-    size_t cap = 0;
-    std::vector<std::pair<size_t, size_t>> live;   // (offset, bytes), in allocation order
-    size_t top() const { return live.empty() ? 0 : live.back().first + live.back().second; }
+    struct Block { char *base; size_t cap; int live; };
+    std::vector<Block> blocks;                       // blocks.back() is the current one
+    size_t top = 0;                                  // bump offset in the current block
+    std::map<char *, size_t> live;                   // workspace -> index of its block
 };
 std::map<std::pair<int, hipStream_t>, Arena> g_arenas;
-
-hipError_t pool_of(int dev, hipMemPool_t *pool) {   // (g_pool_mu held)
-    if (!g_pool[dev]) {
-        hipMemPoolProps props{};
-        props.allocType = hipMemAllocationTypePinned;
-        props.handleTypes = hipMemHandleTypeNone;
-        props.location.type = hipMemLocationTypeDevice;
-        props.location.id = dev;
-        hipError_t e = hipMemPoolCreate(&g_pool[dev], &props);
-        if (e != hipSuccess) { g_pool[dev] = nullptr; return e; }
-        const char *k = getenv("RBH_POOL_KEEP_BYTES");
-        uint64_t keep = k ? strtoull(k, nullptr, 10) : UINT64_MAX;
-        (void)hipMemPoolSetAttribute(g_pool[dev], hipMemPoolAttrReleaseThreshold, &keep);
-    }
-    *pool = g_pool[dev];
-    return hipSuccess;
-}
+constexpr size_t WS_ALIGN = 256;
+constexpr size_t WS_MIN_BLOCK = (size_t)64 << 20;
 }  // namespace
 hipError_t ws_alloc(void **p, size_t bytes, hipStream_t s) {
+    *p = nullptr;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-    // diagnostics (the pool-trim study): RBH_WS_MODE=legacy takes workspaces from
-    // hipMalloc; =sync synchronises the stream after each pool allocation (no arena in either)
-    static const int mode = [] {
-        const char *m = getenv("RBH_WS_MODE");
-        return !m ? 0 : (!strcmp(m, "legacy") ? 1 : (!strcmp(m, "sync") ? 2 : 0));
-    }();
-    if (mode == 1) return hipMalloc(p, bytes);
-    std::lock_guard<std::mutex> lk(g_pool_mu);
-    hipMemPool_t pool;
-    e = pool_of(dev, &pool);
-    if (e != hipSuccess) return e;
-    if (mode == 2) {
-        e = hipMallocFromPoolAsync(p, bytes, pool, s);
-        return e == hipSuccess ? hipStreamSynchronize(s) : e;
-    }
-    const size_t need = (bytes + 255) & ~(size_t)255;
+    const size_t need = (bytes + WS_ALIGN - 1) & ~(WS_ALIGN - 1);
+    std::lock_guard<std::mutex> lk(g_ws_mu);
     Arena &a = g_arenas[{dev, s}];
-    if (a.base && a.top() + need <= a.cap) {
-        a.live.emplace_back(a.top(), need);
-        *p = a.base + a.live.back().first;
-        return hipSuccess;
-    }
-    if (a.live.empty()) {   // grow: the old block is released in stream order
-        const size_t cap = need > 2 * a.cap ? need : 2 * a.cap;
+    if (a.blocks.empty() || a.top + need > a.blocks.back().cap) {
+        const size_t last = a.blocks.empty() ? 0 : a.blocks.back().cap;
+        size_t cap = 2 * last > WS_MIN_BLOCK ? 2 * last : WS_MIN_BLOCK;
+        if (cap < need) cap = need;
         char *nb = nullptr;
-        e = hipMallocFromPoolAsync((void **)&nb, cap, pool, s);
+        e = hipMalloc((void **)&nb, cap);
         if (e != hipSuccess) return e;
-        if (a.base) (void)hipFreeAsync(a.base, s);
-        a.base = nb;
-        a.cap = cap;
-        a.live.emplace_back(0, need);
-        *p = a.base;
-        return hipSuccess;
+        // retired blocks without live workspaces go now (hipFree synchronises the device)
+        for (size_t i = a.blocks.size(); i-- > 0;)
+            if (a.blocks[i].live == 0) {
+                (void)hipFree(a.blocks[i].base);
+                a.blocks.erase(a.blocks.begin() + (ptrdiff_t)i);
+                for (auto &w : a.live)
+                    if (w.second > i) --w.second;
+            }
+        a.blocks.push_back({nb, cap, 0});
+        a.top = 0;
     }
-    return hipMallocFromPoolAsync(p, bytes, pool, s);
+    Arena::Block &b = a.blocks.back();
+    char *q = b.base + a.top;
+    a.top += need;
+    b.live++;
+    a.live[q] = a.blocks.size() - 1;
+    *p = q;
+    return hipSuccess;
 }
 hipError_t ws_free(void *p, hipStream_t s) {
-    static const bool legacy = [] { const char *m = getenv("RBH_WS_MODE"); return m && !strcmp(m, "legacy"); }();
     if (!p) return hipSuccess;
-    if (legacy) {
-        hipError_t e = hipStreamSynchronize(s);
-        return e == hipSuccess ? hipFree(p) : e;
-    }
     int dev = 0;
-    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
-        std::lock_guard<std::mutex> lk(g_pool_mu);
-        auto it = g_arenas.find({dev, s});
-        if (it != g_arenas.end() && it->second.base && (char *)p >= it->second.base &&
-            (char *)p < it->second.base + it->second.cap) {
-            Arena &a = it->second;
-            const size_t off = (size_t)((char *)p - a.base);
-            for (size_t i = a.live.size(); i-- > 0;)
-                if (a.live[i].first == off) { a.live.erase(a.live.begin() + (ptrdiff_t)i); break; }
-            return hipSuccess;
-        }
-    }
-    return hipFreeAsync(p, s);
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    auto it = g_arenas.find({dev, s});
+    if (it == g_arenas.end()) return hipErrorInvalidValue;
+    Arena &a = it->second;
+    auto w = a.live.find((char *)p);
+    if (w == a.live.end()) return hipErrorInvalidValue;
+    const size_t bi = w->second;
+    a.live.erase(w);
+    a.blocks[bi].live--;
+    // the current block empties: bump from its start again (stream order protects the reuse)
+    if (bi + 1 == a.blocks.size() && a.blocks[bi].live == 0) a.top = 0;
+    return hipSuccess;
 }
 }  // namespace rbh
 
