@@ -955,20 +955,25 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
     const int grow = r * KB32;                    // + 16 * a * KB32
     const int mrow = (16 * FB * wave + r) * KB32;  // + 16 * c * KB32
     const int sw = sw32(r);
-    // Waves w and w + 4 share a SIMD and take the step's draw and MFMAs in opposite order, so one
-    // feeds the matrix pipe while the other draws (two copies of the loop, one order each).
-    auto k_loop = [&](auto mfma_first_tag) {
-    constexpr bool MFMA_FIRST = decltype(mfma_first_tag)::value;
+    // Waves w and w + 4 share a SIMD and place the step's draw at different points of their MFMA
+    // stream (POS 0: before the MFMAs, 1: between the two halves, 2: after), so one feeds the
+    // matrix pipe while the other draws (one copy of the loop per placement).
+    auto k_loop = [&](auto pos_tag) {
+    constexpr int POS = decltype(pos_tag)::value;
     for (int64_t kt = kt0; kt < kt1; ++kt) {
         const int cur = (int)((kt - kt0) & 1);
         const T *Mc = lds + cur * MS;
         const T *Gc = lds + 2 * MS + cur * GS;
         const int64_t kn = (kt + 1) * KB32;
         rload(kn, 0);
-        if (!MFMA_FIRST) draw(kt + 1);
+        if (POS == 0) draw(kt + 1);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            if (h == 1) { rstore(cur ^ 1, 0); rload(kn, 1); }
+            if (h == 1) {
+                rstore(cur ^ 1, 0);
+                rload(kn, 1);
+                if (POS == 1) draw(kt + 1);
+            }
             const int slot = 4 * ((2 * g + h) ^ sw);
             v4f gf[FA], mf[FB];
 #pragma unroll
@@ -984,17 +989,20 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
                         acc[a][c] = GX ? Mfma<T>::mma(mf[c][s], gf[a][s], acc[a][c])
                                        : Mfma<T>::mma(gf[a][s], mf[c][s], acc[a][c]);
         }
-        if (MFMA_FIRST) draw(kt + 1);
+        if (POS == 2) draw(kt + 1);
         gstore(cur ^ 1);
         rstore(cur ^ 1, 1);
         __syncthreads();
     }
     };
-#ifndef RBH_W32_PHASE
-#define RBH_W32_PHASE 1
+#ifndef RBH_W32_POS_A
+#define RBH_W32_POS_A 2
 #endif
-    if (!RBH_W32_PHASE || ((wave >> 2) & 1) == 0) k_loop(std::true_type{});
-    else k_loop(std::false_type{});
+#ifndef RBH_W32_POS_B
+#define RBH_W32_POS_B 0
+#endif
+    if (((wave >> 2) & 1) == 0) k_loop(std::integral_constant<int, RBH_W32_POS_A>{});
+    else k_loop(std::integral_constant<int, RBH_W32_POS_B>{});
 
     T *C = SPLIT ? (T *)p.partial + z * p.M * p.N : (T *)p.C;
     const int64_t ldc = SPLIT ? p.M : p.ldc;
