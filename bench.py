@@ -348,7 +348,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": dtype,
-            "data": "synthetic (A ~ Gaussian DenseDist(m,n) key 99 generated on device; S regenerated in-kernel)",
+            "data": ("synthetic (A ~ Gaussian DenseDist(m,n) key 99 generated on device; "
+                     + ("the SASO operator sampled in every call)" if kind == "saso" else
+                        "the operator window drawn on the device in every call)")),
             "config": {"workload": {"c1": "Gaussian skge fp64 d=128 A 4096^2 (BASELINE configs[0], the reference's CPU case)",
                                     "c2": "Gaussian skge fp64 (BASELINE configs[1])",
                                     "ns": "Gaussian skge fp64 north-star",

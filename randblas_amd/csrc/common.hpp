@@ -54,6 +54,9 @@ struct GemmProblem {
     // or k >= o (2 full, 4 packed ptr[(k - o) + o*tri_n - o(o-1)/2]); the rest is its mirror (k, o).
     int tri;
     int64_t tri_n;
+    // The generated operand materialised by the launcher (wide kernels, launch_gemm): element (o, k)
+    // at gmat[o * K + k]; null = drawn inside the kernel.
+    const void *gmat;
 };
 
 // Expand a one-triangle operand (GemmProblem::tri conventions, n x n) into full storage

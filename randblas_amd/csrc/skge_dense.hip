@@ -536,7 +536,7 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 // element (o, k) outside it is the stored (k, o). A K step's 512 x 16 tile is then wholly inside
 // the triangle (loaded as usual), wholly outside (loaded from the mirror tile, which is contiguous
 // along o, and transposed into the LDS image), or straddles the diagonal (per-element select).
-template <int GK, int FAMILY, bool GX, int TRI, bool SPLIT>
+template <int GK, int FAMILY, bool GX, int TRI, bool SPLIT, bool GMAT>
 __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
     typedef double T;
     // 8 waves = WGW (along the generated dimension) x WMW (along the memory dimension); each wave
@@ -722,6 +722,18 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
             for (int e = 0; e < 4; ++e) G[(4 * q + e) * LDG + k] = gv[e];
         }
     };
+    // GMAT: the 64 x 16 generated tile comes from the materialised operand (launch_gemm): one 16-B
+    // vector per thread, row tid >> 3 (clamped to the operand: rows past it only feed discarded
+    // outputs), k pair tid & 7, into the same LDS rows the draw fills
+    v2_t gm;
+    const T *gmrow = (const T *)p.gmat + (go0 + (tid >> 3) < gnO ? go0 + (tid >> 3) : gnO - 1) * p.K + 2 * (tid & 7);
+    auto gload = [&](int64_t kt) {
+        const int64_t k0 = kt * BK < p.K ? kt * BK : p.K - BK;
+        gm = *reinterpret_cast<const v2_t *>(gmrow + k0);
+    };
+    auto gstore_m = [&](int st) {
+        *reinterpret_cast<v2_t *>(lds + 2 * MS + st * GS + (tid >> 3) * LDG + 2 * (tid & 7)) = gm;
+    };
 
     acc_t acc[FA][FB];
 #pragma unroll
@@ -740,7 +752,8 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
     } else {
         rload(kt0 * BK, 0); rstore(0, 0); rload(kt0 * BK, 1); rstore(0, 1);
     }
-    if (wave < 4) { draw(kt0); gstore(0); }
+    if (GMAT) { gload(kt0); gstore_m(0); }
+    else if (wave < 4) { draw(kt0); gstore(0); }
     __syncthreads();
 
     // fragment addresses (doubles) relative to the stage base
@@ -757,7 +770,8 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
         const int cn = tclass(kn);
         if (TRI) rload_tri(kn, 0, cn);
         else rload(kn, 0);
-        if (wave < 4) draw(kt + 1);
+        if (GMAT) gload(kt + 1);
+        else if (wave < 4) draw(kt + 1);
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             if (s == 2) {
@@ -777,7 +791,8 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
                 for (int c = 0; c < FB; ++c)
                     acc[a][c] = GX ? Mfma<T>::mma(mf[c], gf[a], acc[a][c]) : Mfma<T>::mma(gf[a], mf[c], acc[a][c]);
         }
-        if (wave < 4) gstore(cur ^ 1);
+        if (GMAT) gstore_m(cur ^ 1);
+        else if (wave < 4) gstore(cur ^ 1);
         if (TRI) rstore_tri(cur ^ 1, 1, cn);
         else rstore(cur ^ 1, 1);
         __syncthreads();
@@ -834,7 +849,7 @@ constexpr int KB32 = 32;
 // group land in different bank quads)
 __device__ __forceinline__ int sw32(int o) { return ((o >> 1) & 1) | ((o >> 1) & 4); }
 
-template <int GK, int FAMILY, bool GX, bool SPLIT>
+template <int GK, int FAMILY, bool GX, bool SPLIT, bool GMAT>
 __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
     typedef float T;
     constexpr int BG = 64, BMM = 512, WMW = 8;
@@ -919,9 +934,18 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
             }
         }
     };
+    // GMAT: the 64 x 32 tile from the materialised operand, one 16-B vector per thread (row tid >> 3
+    // clamped, k quad tid & 7), stored as the GEN_OK draw is
+    const T *gmrow = (const T *)p.gmat + (go0 + (tid >> 3) < gnO ? go0 + (tid >> 3) : gnO - 1) * p.K + 4 * (tid & 7);
+    auto gload = [&](int64_t kt) {
+        const int64_t k0 = kt * KB32 < p.K ? kt * KB32 : p.K - KB32;
+        const v4f x = *reinterpret_cast<const v4f *>(gmrow + k0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) gv[e] = x[e];
+    };
     auto gstore = [&](int st) {
         T *G = lds + 2 * MS + st * GS;
-        if (GK == GEN_OK) {
+        if (GK == GEN_OK || GMAT) {
             const int o = tid >> 3, q = tid & 7;
             v4f x;
 #pragma unroll
@@ -948,7 +972,9 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
     const int64_t kt0 = SPLIT ? z * per : 0, kt1 = SPLIT ? (kt0 + per < nk ? kt0 + per : nk) : nk;
     __syncthreads();   // tab
     rload(kt0 * KB32, 0); rstore(0, 0); rload(kt0 * KB32, 1); rstore(0, 1);
-    draw(kt0); gstore(0);
+    if (GMAT) gload(kt0);
+    else draw(kt0);
+    gstore(0);
     __syncthreads();
 
     // fragment rows (floats, relative to the stage base); the swizzle of rows 16 a + r is sw32(r)
@@ -966,13 +992,14 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
         const T *Gc = lds + 2 * MS + cur * GS;
         const int64_t kn = (kt + 1) * KB32;
         rload(kn, 0);
-        if (POS == 0) draw(kt + 1);
+        if (GMAT) gload(kt + 1);
+        else if (POS == 0) draw(kt + 1);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             if (h == 1) {
                 rstore(cur ^ 1, 0);
                 rload(kn, 1);
-                if (POS == 1) draw(kt + 1);
+                if (!GMAT && POS == 1) draw(kt + 1);
             }
             const int slot = 4 * ((2 * g + h) ^ sw);
             v4f gf[FA], mf[FB];
@@ -989,7 +1016,7 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
                         acc[a][c] = GX ? Mfma<T>::mma(mf[c][s], gf[a][s], acc[a][c])
                                        : Mfma<T>::mma(gf[a][s], mf[c][s], acc[a][c]);
         }
-        if (POS == 2) draw(kt + 1);
+        if (!GMAT && POS == 2) draw(kt + 1);
         gstore(cur ^ 1);
         rstore(cur ^ 1, 1);
         __syncthreads();
@@ -1132,6 +1159,67 @@ static bool fused_ok(const GemmProblem &p) {
     return mode == 2 && (g.pc0 & 3) == 0;
 }
 
+// ------------------------------------------------------------------------------------------
+// Materialised generated operand (the reference's own order: fill_dense of submat(S), then GEMM)
+// ------------------------------------------------------------------------------------------
+// A wide kernel that draws its operator tile regenerates every entry once per 512-row tile of the
+// memory operand: n / 512 = 32 times at C2, 64 at C4. When that factor reaches MAT_MIN_TILES the
+// launcher draws the window once into a workspace, gmat[o * K + k] (one Philox call per 4 entries,
+// the same samples as the in-kernel draw), and the wide kernel loads its tile from there (GMAT)
+// instead of drawing it. The LDS image and the MFMA order are unchanged, so the results are
+// bitwise those of the drawing kernel. Measured (C2 with the draw removed: 8.98 -> 8.41 ms) before
+// building it; RBH_NO_MAT=1 keeps the in-kernel draw.
+constexpr int64_t MAT_MIN_TILES = 4;
+constexpr int64_t MAT_MAX_BYTES = (int64_t)8 << 30;
+
+template <typename T, int GK, int FAMILY>
+__global__ __launch_bounds__(256) void gen_fill_kernel(const GenOperand g, int64_t gnO, int64_t K, T *buf) {
+    // one Philox call per thread and step: GEN_OK 4 consecutive k of row a; GEN_OO 4 consecutive
+    // outer indices at k = a. Both: counter offset (pr0 + a) * stride + pc0 / 4 + q (pc0 % 4 == 0).
+    const int64_t per = GK == GEN_OK ? K / 4 : (gnO + 3) / 4;
+    const int64_t total = (GK == GEN_OK ? gnO : K) * per;
+    typedef T v4_t __attribute__((ext_vector_type(4)));
+    for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < total; c += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t a = c / per, q = c - a * per;
+        uint32_t cc[4];
+        rb::ctr_add(g.ctr, (uint64_t)(g.pr0 + a) * g.stride + (uint64_t)(g.pc0 >> 2) + (uint64_t)q, cc);
+        const rb::u32x4 w = rb::philox4x32<10>(cc[0], cc[1], cc[2], cc[3], g.key[0], g.key[1]);
+        float sm[4];
+        rb::sample4<FAMILY>(w, sm);
+        v4_t v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = FAMILY == rb::UNIFORM ? (T)sm[e] * (T)g.scale : (T)sm[e];
+        if (GK == GEN_OK) {
+            *reinterpret_cast<v4_t *>(buf + a * K + 4 * q) = v;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (4 * q + e < gnO) buf[(4 * q + e) * K + a] = v[e];
+        }
+    }
+}
+
+// the generated operand of p (GX: X) drawn into a workspace; *buf stays null when the kernel
+// should draw in place (few memory tiles, too large, or RBH_NO_MAT=1)
+template <typename T, int GK, int FAMILY, bool GX>
+static hipError_t materialise(const GemmProblem &p, void **buf, hipStream_t s) {
+    static const bool off = [] { const char *e = getenv("RBH_NO_MAT"); return e && e[0] == '1'; }();
+    *buf = nullptr;
+    const int64_t gnO = GX ? p.M : p.N, mnO = GX ? p.N : p.M;
+    const int64_t bytes = gnO * p.K * (int64_t)sizeof(T);
+    if (off || (mnO + 511) / 512 < MAT_MIN_TILES || bytes > MAT_MAX_BYTES || bytes <= 0) return hipSuccess;
+    hipError_t e = ws_alloc(buf, (size_t)bytes, s);
+    if (e != hipSuccess) return e;
+    const GenOperand &g = GX ? p.xg : p.yg;
+    const int64_t calls = (GK == GEN_OK ? gnO * (p.K / 4) : p.K * ((gnO + 3) / 4));
+    int64_t blocks = (calls + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL((gen_fill_kernel<T, GK, FAMILY>), dim3((unsigned)blocks), dim3(256), 0, s, g, gnO, p.K, (T *)*buf);
+    e = hipGetLastError();
+    if (e != hipSuccess) { (void)ws_free(*buf, s); *buf = nullptr; }
+    return e;
+}
+
 template <int GK, int FAMILY, bool GX, int TRI = 0>
 static hipError_t launch_wide(const GemmProblem &p, hipStream_t s) {
     typedef double T;
@@ -1143,13 +1231,23 @@ static hipError_t launch_wide(const GemmProblem &p, hipStream_t s) {
     q.splitk = split;
     q.partial = nullptr;
     hipError_t e;
+    void *gm = nullptr;
+    e = materialise<T, GK, FAMILY, GX>(p, &gm, s);
+    if (e != hipSuccess) return e;
+    q.gmat = gm;
     if (split > 1) {
         e = ws_alloc(&q.partial, sizeof(T) * (size_t)split * p.M * p.N, s);
-        if (e != hipSuccess) return e;
+        if (e != hipSuccess) { if (gm) (void)ws_free(gm, s); return e; }
     }
     timing_begin(s);
-    if (split > 1) hipLaunchKernelGGL((skge_wide_kernel<GK, FAMILY, GX, TRI, true>), dim3((unsigned)(nb * split)), dim3(512), 0, s, q);
-    else hipLaunchKernelGGL((skge_wide_kernel<GK, FAMILY, GX, TRI, false>), dim3((unsigned)nb), dim3(512), 0, s, q);
+    // (a materialised operand needs neither GK nor FAMILY: one instantiation per GX / TRI / SPLIT)
+    if (gm) {
+        if (split > 1) hipLaunchKernelGGL((skge_wide_kernel<GEN_OK, rb::GAUSSIAN, GX, TRI, true, true>), dim3((unsigned)(nb * split)), dim3(512), 0, s, q);
+        else hipLaunchKernelGGL((skge_wide_kernel<GEN_OK, rb::GAUSSIAN, GX, TRI, false, true>), dim3((unsigned)nb), dim3(512), 0, s, q);
+    } else {
+        if (split > 1) hipLaunchKernelGGL((skge_wide_kernel<GK, FAMILY, GX, TRI, true, false>), dim3((unsigned)(nb * split)), dim3(512), 0, s, q);
+        else hipLaunchKernelGGL((skge_wide_kernel<GK, FAMILY, GX, TRI, false, false>), dim3((unsigned)nb), dim3(512), 0, s, q);
+    }
     e = hipGetLastError();
     if (split > 1 && e == hipSuccess) {
         hipLaunchKernelGGL(splitk_reduce_kernel<T>, dim3(2048), dim3(256), 0, s, p.M, p.N, split,
@@ -1159,6 +1257,10 @@ static hipError_t launch_wide(const GemmProblem &p, hipStream_t s) {
     timing_end(s);
     if (split > 1) {
         const hipError_t e2 = ws_free(q.partial, s);
+        if (e == hipSuccess) e = e2;
+    }
+    if (gm) {
+        const hipError_t e2 = ws_free(gm, s);
         if (e == hipSuccess) e = e2;
     }
     return e;
@@ -1189,13 +1291,22 @@ static hipError_t launch_wide32(const GemmProblem &p, hipStream_t s) {
     q.splitk = split;
     q.partial = nullptr;
     hipError_t e;
+    void *gm = nullptr;
+    e = materialise<T, GK, FAMILY, GX>(p, &gm, s);
+    if (e != hipSuccess) return e;
+    q.gmat = gm;
     if (split > 1) {
         e = ws_alloc(&q.partial, sizeof(T) * (size_t)split * p.M * p.N, s);
-        if (e != hipSuccess) return e;
+        if (e != hipSuccess) { if (gm) (void)ws_free(gm, s); return e; }
     }
     timing_begin(s);
-    if (split > 1) hipLaunchKernelGGL((skge_wide32_kernel<GK, FAMILY, GX, true>), dim3((unsigned)(nb * split)), dim3(512), 0, s, q);
-    else hipLaunchKernelGGL((skge_wide32_kernel<GK, FAMILY, GX, false>), dim3((unsigned)nb), dim3(512), 0, s, q);
+    if (gm) {
+        if (split > 1) hipLaunchKernelGGL((skge_wide32_kernel<GEN_OK, rb::GAUSSIAN, GX, true, true>), dim3((unsigned)(nb * split)), dim3(512), 0, s, q);
+        else hipLaunchKernelGGL((skge_wide32_kernel<GEN_OK, rb::GAUSSIAN, GX, false, true>), dim3((unsigned)nb), dim3(512), 0, s, q);
+    } else {
+        if (split > 1) hipLaunchKernelGGL((skge_wide32_kernel<GK, FAMILY, GX, true, false>), dim3((unsigned)(nb * split)), dim3(512), 0, s, q);
+        else hipLaunchKernelGGL((skge_wide32_kernel<GK, FAMILY, GX, false, false>), dim3((unsigned)nb), dim3(512), 0, s, q);
+    }
     e = hipGetLastError();
     if (split > 1 && e == hipSuccess) {
         hipLaunchKernelGGL(splitk_reduce_kernel<T>, dim3(2048), dim3(256), 0, s, p.M, p.N, split,
@@ -1205,6 +1316,10 @@ static hipError_t launch_wide32(const GemmProblem &p, hipStream_t s) {
     timing_end(s);
     if (split > 1) {
         const hipError_t e2 = ws_free(q.partial, s);
+        if (e == hipSuccess) e = e2;
+    }
+    if (gm) {
+        const hipError_t e2 = ws_free(gm, s);
         if (e == hipSuccess) e = e2;
     }
     return e;
