@@ -30,6 +30,15 @@
 namespace rbh {
 
 constexpr int BK = 16;
+// waves that load a materialised operator tile in the wide kernels (see skge_wide_kernel)
+// (measured, same box, both orders: f64 C2 8 waves 8.49-8.53 ms, 1 8.52-8.54, 2 8.57-8.59, 4 8.61-8.63;
+// f32 C4 4 waves 4.36 ms, 2 4.51-4.53, 1 and 8 4.65-4.67)
+#ifndef RBH_GMAT_W
+#define RBH_GMAT_W 8
+#endif
+#ifndef RBH_GMAT32_W
+#define RBH_GMAT32_W 4
+#endif
 
 template <typename T> struct Mfma;
 template <> struct Mfma<double> {
@@ -722,17 +731,27 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
             for (int e = 0; e < 4; ++e) G[(4 * q + e) * LDG + k] = gv[e];
         }
     };
-    // GMAT: the 64 x 16 generated tile comes from the materialised operand (launch_gemm): one 16-B
-    // vector per thread, row tid >> 3 (clamped to the operand: rows past it only feed discarded
-    // outputs), k pair tid & 7, into the same LDS rows the draw fills
-    v2_t gm;
-    const T *gmrow = (const T *)p.gmat + (go0 + (tid >> 3) < gnO ? go0 + (tid >> 3) : gnO - 1) * p.K + 2 * (tid & 7);
+    // GMAT: the 64 x 16 generated tile comes from the materialised operand (launch_gemm), rows
+    // clamped to the operand (rows past it only feed discarded outputs), into the same LDS rows the
+    // draw fills.
+    constexpr int GMAT_W = RBH_GMAT_W;
+    // The first GMAT_W waves load the tile, 8 / GMAT_W vectors per lane (lanes per row = GMAT_W);
+    // the other waves only feed the matrix pipe
+    constexpr int VPL = 8 / GMAT_W;
+    v2_t gmv[VPL];
+    const int grw = (tid & (64 * GMAT_W - 1)) / GMAT_W, gvc = (tid % GMAT_W) * VPL;
+    const T *gmrow = (const T *)p.gmat + (go0 + grw < gnO ? go0 + grw : gnO - 1) * p.K + 2 * gvc;
     auto gload = [&](int64_t kt) {
+        if (wave >= GMAT_W) return;
         const int64_t k0 = kt * BK < p.K ? kt * BK : p.K - BK;
-        gm = *reinterpret_cast<const v2_t *>(gmrow + k0);
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) gmv[v] = *reinterpret_cast<const v2_t *>(gmrow + k0 + 2 * v);
     };
     auto gstore_m = [&](int st) {
-        *reinterpret_cast<v2_t *>(lds + 2 * MS + st * GS + (tid >> 3) * LDG + 2 * (tid & 7)) = gm;
+        if (wave >= GMAT_W) return;
+        T *dst = lds + 2 * MS + st * GS + grw * LDG + 2 * gvc;
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) *reinterpret_cast<v2_t *>(dst + 2 * v) = gmv[v];
     };
 
     acc_t acc[FA][FB];
@@ -771,7 +790,7 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
         if (TRI) rload_tri(kn, 0, cn);
         else rload(kn, 0);
         if (GMAT) gload(kt + 1);
-        else if (wave < 4) draw(kt + 1);
+        else if (!GMAT && wave < 4) draw(kt + 1);
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             if (s == 2) {
@@ -934,18 +953,28 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
             }
         }
     };
-    // GMAT: the 64 x 32 tile from the materialised operand, one 16-B vector per thread (row tid >> 3
-    // clamped, k quad tid & 7), stored as the GEN_OK draw is
-    const T *gmrow = (const T *)p.gmat + (go0 + (tid >> 3) < gnO ? go0 + (tid >> 3) : gnO - 1) * p.K + 4 * (tid & 7);
+    // GMAT: the 64 x 32 tile from the materialised operand (rows clamped), loaded by the first
+    // GMAT_W waves, 8 / GMAT_W vectors per lane, into the swizzled rows the GEN_OK draw fills
+    constexpr int GMAT_W = RBH_GMAT32_W;
+    constexpr int VPL = 8 / GMAT_W;
+    v4f gmv[VPL];
+    const int grw = (tid & (64 * GMAT_W - 1)) / GMAT_W, gvc = (tid % GMAT_W) * VPL;
+    const T *gmrow = (const T *)p.gmat + (go0 + grw < gnO ? go0 + grw : gnO - 1) * p.K + 4 * gvc;
     auto gload = [&](int64_t kt) {
+        if (wave >= GMAT_W) return;
         const int64_t k0 = kt * KB32 < p.K ? kt * KB32 : p.K - KB32;
-        const v4f x = *reinterpret_cast<const v4f *>(gmrow + k0);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) gv[e] = x[e];
+        for (int v = 0; v < VPL; ++v) gmv[v] = *reinterpret_cast<const v4f *>(gmrow + k0 + 4 * v);
+    };
+    auto gstore_m = [&](int st) {
+        if (wave >= GMAT_W) return;
+        T *G = lds + 2 * MS + st * GS + grw * KB32;
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) *reinterpret_cast<v4f *>(G + 4 * ((gvc + v) ^ sw32(grw))) = gmv[v];
     };
     auto gstore = [&](int st) {
         T *G = lds + 2 * MS + st * GS;
-        if (GK == GEN_OK || GMAT) {
+        if (GK == GEN_OK) {
             const int o = tid >> 3, q = tid & 7;
             v4f x;
 #pragma unroll
@@ -972,9 +1001,8 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
     const int64_t kt0 = SPLIT ? z * per : 0, kt1 = SPLIT ? (kt0 + per < nk ? kt0 + per : nk) : nk;
     __syncthreads();   // tab
     rload(kt0 * KB32, 0); rstore(0, 0); rload(kt0 * KB32, 1); rstore(0, 1);
-    if (GMAT) gload(kt0);
-    else draw(kt0);
-    gstore(0);
+    if (GMAT) { gload(kt0); gstore_m(0); }
+    else { draw(kt0); gstore(0); }
     __syncthreads();
 
     // fragment rows (floats, relative to the stage base); the swizzle of rows 16 a + r is sw32(r)
@@ -1017,7 +1045,8 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
                                        : Mfma<T>::mma(gf[a][s], mf[c][s], acc[a][c]);
         }
         if (!GMAT && POS == 2) draw(kt + 1);
-        gstore(cur ^ 1);
+        if (GMAT) gstore_m(cur ^ 1);
+        else gstore(cur ^ 1);
         rstore(cur ^ 1, 1);
         __syncthreads();
     }
@@ -1235,6 +1264,16 @@ static hipError_t launch_wide(const GemmProblem &p, hipStream_t s) {
     e = materialise<T, GK, FAMILY, GX>(p, &gm, s);
     if (e != hipSuccess) return e;
     q.gmat = gm;
+#ifdef RBH_MAT_GENERIC
+    if (gm && TRI == 0 && split == 1) {   // experiment: the 128 x 256 generic kernel on two memory operands
+        GemmProblem r = p;
+        MemOperand m{gm, p.K, 1};
+        if (GX) { r.xkind = MEM; r.xm = m; r.xmode = 2; } else { r.ykind = MEM; r.ym = m; r.ymode = 2; }
+        e = launch_one<T, MEM, MEM, rb::GAUSSIAN, 128, 256, 2, 4>(r, s);
+        const hipError_t e2 = ws_free(gm, s);
+        return e != hipSuccess ? e : e2;
+    }
+#endif
     if (split > 1) {
         e = ws_alloc(&q.partial, sizeof(T) * (size_t)split * p.M * p.N, s);
         if (e != hipSuccess) { if (gm) (void)ws_free(gm, s); return e; }
