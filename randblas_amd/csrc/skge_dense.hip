@@ -735,6 +735,10 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
     // clamped to the operand (rows past it only feed discarded outputs), into the same LDS rows the
     // draw fills.
     constexpr int GMAT_W = RBH_GMAT_W;
+    // The wave test stays in the code even when every wave loads (GMAT_W = 8, the compiler cannot
+    // prove wave < 8) for TRI == 0: the split basic block schedules C2 at 8.49-8.53 ms against 8.81
+    // without it, while the one-triangle kernels run faster without it (C5p 4.97 against 5.90 ms).
+    constexpr bool GMAT_BR = GMAT_W < 8 || TRI == 0;
     // The first GMAT_W waves load the tile, 8 / GMAT_W vectors per lane (lanes per row = GMAT_W);
     // the other waves only feed the matrix pipe
     constexpr int VPL = 8 / GMAT_W;
@@ -742,13 +746,13 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
     const int grw = (tid & (64 * GMAT_W - 1)) / GMAT_W, gvc = (tid % GMAT_W) * VPL;
     const T *gmrow = (const T *)p.gmat + (go0 + grw < gnO ? go0 + grw : gnO - 1) * p.K + 2 * gvc;
     auto gload = [&](int64_t kt) {
-        if (wave >= GMAT_W) return;
+        if (GMAT_BR && wave >= GMAT_W) return;
         const int64_t k0 = kt * BK < p.K ? kt * BK : p.K - BK;
 #pragma unroll
         for (int v = 0; v < VPL; ++v) gmv[v] = *reinterpret_cast<const v2_t *>(gmrow + k0 + 2 * v);
     };
     auto gstore_m = [&](int st) {
-        if (wave >= GMAT_W) return;
+        if (GMAT_BR && wave >= GMAT_W) return;
         T *dst = lds + 2 * MS + st * GS + grw * LDG + 2 * gvc;
 #pragma unroll
         for (int v = 0; v < VPL; ++v) *reinterpret_cast<v2_t *>(dst + 2 * v) = gmv[v];
@@ -961,13 +965,13 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
     const int grw = (tid & (64 * GMAT_W - 1)) / GMAT_W, gvc = (tid % GMAT_W) * VPL;
     const T *gmrow = (const T *)p.gmat + (go0 + grw < gnO ? go0 + grw : gnO - 1) * p.K + 4 * gvc;
     auto gload = [&](int64_t kt) {
-        if (wave >= GMAT_W) return;
+        if (GMAT_W < 8 && wave >= GMAT_W) return;
         const int64_t k0 = kt * KB32 < p.K ? kt * KB32 : p.K - KB32;
 #pragma unroll
         for (int v = 0; v < VPL; ++v) gmv[v] = *reinterpret_cast<const v4f *>(gmrow + k0 + 4 * v);
     };
     auto gstore_m = [&](int st) {
-        if (wave >= GMAT_W) return;
+        if (GMAT_W < 8 && wave >= GMAT_W) return;
         T *G = lds + 2 * MS + st * GS + grw * KB32;
 #pragma unroll
         for (int v = 0; v < VPL; ++v) *reinterpret_cast<v4f *>(G + 4 * ((gvc + v) ^ sw32(grw))) = gmv[v];
