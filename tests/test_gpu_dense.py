@@ -264,3 +264,21 @@ def test_row_shards_reassemble(cuda):
         rb.sketch_general_left("C", "N", "N", d // G, n, m, 1.0, S, A, m, 0.0, part, d // G, ro_s=g * d // G)
         parts.append(host(part).reshape((d // G, n), order="F"))
     assert np.array_equal(np.vstack(parts), full)
+
+
+# Memory operands spanning >= 4 wide tiles (here 2100 outer indices) take the materialised-operator
+# kernels (skge_dense.hip: gen_fill_kernel + the GMAT wide kernels): generated rows not a multiple of
+# 64, a ragged last tile, a submatrix window, both families and major axes, f64 and f32 (K = 256 is a
+# multiple of both step depths), left and right sketches.
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("layout", ["C", "R"])
+@pytest.mark.parametrize("fam,maj", [("G", "L"), ("G", "S"), ("U", "L")])
+def test_lskge3_materialised(cuda, dtype, layout, fam, maj):
+    check_left(cuda, layout, "N", "N", 100, 2100, 256, 1.5, 0.5, 120, 300, 8, 4, dtype, fam=fam, maj=maj)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("layout", ["C", "R"])
+@pytest.mark.parametrize("fam,maj", [("G", "L"), ("U", "S")])
+def test_rskge3_materialised(cuda, dtype, layout, fam, maj):
+    check_right(cuda, layout, "N", "N", 2100, 100, 256, -0.5, 0.0, 300, 120, 4, 8, dtype, fam=fam, maj=maj)
