@@ -916,7 +916,11 @@ struct SdAcc {
 // is toggled once per four adds (the sign flips are done before the section), each index write
 // followed by its M0 wait state (section 4). LDS reads of the walk stay in flight across the
 // section: index mode relocates the VGPR operands of VALU instructions, not memory returns.
-__device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t *w, const double *y, uint32_t sgn) {
+// The wait state after each index write is an SALU instruction that does useful work: the shift
+// that extracts a later batch's panel offsets (kn[q] = wn[q] >> 8; index mode does not touch SALU).
+// Against an s_nop there: C3 kernel 0.620 -> 0.612 ms (same box, three alternations).
+__device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t *w, const double *y, uint32_t sgn,
+                                        const uint32_t *wn, uint32_t *kn) {
     double ys[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -928,21 +932,23 @@ __device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t *w, const dou
         asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x78" : "=v"(hi) : "v"((uint32_t)(yb >> 32)), "v"(sgn), "s"(w[q]));
         ys[q] = __builtin_bit_cast(double, (yb & 0xffffffffull) | ((uint64_t)hi << 32));
     }
-    asm volatile("s_set_gpr_idx_on %3, gpr_idx(SRC0,DST)\n\t"
-                 "s_nop 0\n\t"
-                 "v_add_f64 v[32:33], v[32:33], %7\n\t"
-                 "s_set_gpr_idx_idx %4\n\t"
-                 "s_nop 0\n\t"
-                 "v_add_f64 v[32:33], v[32:33], %8\n\t"
-                 "s_set_gpr_idx_idx %5\n\t"
-                 "s_nop 0\n\t"
-                 "v_add_f64 v[32:33], v[32:33], %9\n\t"
-                 "s_set_gpr_idx_idx %6\n\t"
-                 "s_nop 0\n\t"
-                 "v_add_f64 v[32:33], v[32:33], %10\n\t"
+    asm volatile("s_set_gpr_idx_on %7, gpr_idx(SRC0,DST)\n\t"
+                 "s_lshr_b32 %3, %15, 8\n\t"
+                 "v_add_f64 v[32:33], v[32:33], %11\n\t"
+                 "s_set_gpr_idx_idx %8\n\t"
+                 "s_lshr_b32 %4, %16, 8\n\t"
+                 "v_add_f64 v[32:33], v[32:33], %12\n\t"
+                 "s_set_gpr_idx_idx %9\n\t"
+                 "s_lshr_b32 %5, %17, 8\n\t"
+                 "v_add_f64 v[32:33], v[32:33], %13\n\t"
+                 "s_set_gpr_idx_idx %10\n\t"
+                 "s_lshr_b32 %6, %18, 8\n\t"
+                 "v_add_f64 v[32:33], v[32:33], %14\n\t"
                  "s_set_gpr_idx_off"
-                 : "+{v[32:63]}"(acc.a), "+{v[64:95]}"(acc.b), "+{v[96:97]}"(acc.dmy)
-                 : "s"(w[0]), "s"(w[1]), "s"(w[2]), "s"(w[3]), "v"(ys[0]), "v"(ys[1]), "v"(ys[2]), "v"(ys[3])
+                 : "+{v[32:63]}"(acc.a), "+{v[64:95]}"(acc.b), "+{v[96:97]}"(acc.dmy),
+                   "=&s"(kn[0]), "=&s"(kn[1]), "=&s"(kn[2]), "=&s"(kn[3])
+                 : "s"(w[0]), "s"(w[1]), "s"(w[2]), "s"(w[3]), "v"(ys[0]), "v"(ys[1]), "v"(ys[2]), "v"(ys[3]),
+                   "s"(wn[0]), "s"(wn[1]), "s"(wn[2]), "s"(wn[3])
                  : "m0", "scc");
 }
 
@@ -1110,21 +1116,28 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     auto walk_chunk = [&](int64_t ch, int gofs, int ne) {
         const uint32_t L = lanebase + (uint32_t)((ch & 1) * G::PANEL_B);
         auto walk = [&](const uint32_t (&wr)[SD_SW], int nw) {
-            auto issue = [&](int x0, T (&y)[SU_D], uint32_t (&w)[SU_D]) {
+            static_assert(SU_D == 4, "one sd_add4 per step");
+            auto rec = [&](int x) -> uint32_t { return x < SD_SW ? wr[x < SD_SW ? x : 0] : G::PAD; };
+            // records of step x0 / SU_D into w; their panel offsets kf (record >> 8) come from the
+            // update two steps earlier (or are shifted here for the first two steps)
+            auto issue = [&](int x0, T (&y)[SU_D], uint32_t (&w)[SU_D], const uint32_t (&kf)[SU_D]) {
 #pragma unroll
                 for (int q = 0; q < SU_D; ++q) {
-                    w[q] = x0 + q < SD_SW ? wr[x0 + q < SD_SW ? x0 + q : 0] : G::PAD;
-                    y[q] = *reinterpret_cast<const T *>(lbase + (L ^ ((w[q] >> 8) & 0xfffffu)));
+                    w[q] = rec(x0 + q);
+                    y[q] = *reinterpret_cast<const T *>(lbase + (L ^ (kf[q] & 0xfffffu)));
                 }
             };
-            auto update = [&](const T (&y)[SU_D], const uint32_t (&w)[SU_D]) {
-                static_assert(SU_D % 4 == 0, "batched update takes four entries at a time");
+            auto update = [&](const T (&y)[SU_D], const uint32_t (&w)[SU_D], int xn, uint32_t (&kn)[SU_D]) {
+                uint32_t wn[SU_D];
 #pragma unroll
-                for (int g = 0; g < SU_D; g += 4) sd_add4(acc, w + g, y + g, sgn);
+                for (int q = 0; q < SU_D; ++q) wn[q] = rec(xn + q);
+                sd_add4(acc, w, y, sgn, wn, kn);
             };
             T ya[SU_D], yb[SU_D];
-            uint32_t wa[SU_D], wb[SU_D];
-            issue(0, ya, wa);
+            uint32_t wa[SU_D], wb[SU_D], ka[SU_D], kb[SU_D];
+#pragma unroll
+            for (int q = 0; q < SU_D; ++q) { ka[q] = rec(q) >> 8; kb[q] = rec(SU_D + q) >> 8; }
+            issue(0, ya, wa, ka);
             const int nsteps = (nw + SU_D - 1) / SU_D;
             // straight-line walk (a window has at most SD_SW entries): no loop-carried wait state;
             // an issue past the last step reads a stale record's LDS slot, which no add uses
@@ -1132,11 +1145,11 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
 #pragma unroll
             for (int s2 = 0; s2 < MAXS; s2 += 2) {
                 if (s2 >= nsteps) break;
-                issue((s2 + 1) * SU_D, yb, wb);
-                update(ya, wa);
+                issue((s2 + 1) * SU_D, yb, wb, kb);
+                update(ya, wa, (s2 + 2) * SU_D, ka);
                 if (s2 + 1 >= nsteps) break;
-                issue((s2 + 2) * SU_D, ya, wa);
-                update(yb, wb);
+                issue((s2 + 2) * SU_D, ya, wa, ka);
+                update(yb, wb, (s2 + 3) * SU_D, kb);
             }
         };
         for (int done = 0; done < ne; done += SD_SW) {
