@@ -921,17 +921,25 @@ struct SdAcc {
 // Against an s_nop there: C3 kernel 0.620 -> 0.612 ms (same box, three alternations).
 __device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t *w, const double *y, uint32_t sgn,
                                         const uint32_t *wn, uint32_t *kn) {
+    // high word ^= record & 0x80000000 in one VALU each, no SALU mask (C3 kernel 0.600 -> 0.593 ms):
+    // bitop3 0x78 = a ^ (b & c), truth-table index 4a + 2b + c (the compiler's own form of
+    // y ^ (m & s)); sgn is the mask in a VGPR. The four flips share one statement, so the compiler
+    // waits once for the batch's LDS reads instead of once per entry.
+    uint64_t yb[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) yb[q] = __builtin_bit_cast(uint64_t, y[q]);
+    uint32_t hi[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) hi[q] = (uint32_t)(yb[q] >> 32);
+    asm("v_bitop3_b32 %0, %0, %4, %5 bitop3:0x78\n\t"
+        "v_bitop3_b32 %1, %1, %4, %6 bitop3:0x78\n\t"
+        "v_bitop3_b32 %2, %2, %4, %7 bitop3:0x78\n\t"
+        "v_bitop3_b32 %3, %3, %4, %8 bitop3:0x78"
+        : "+v"(hi[0]), "+v"(hi[1]), "+v"(hi[2]), "+v"(hi[3])
+        : "v"(sgn), "s"(w[0]), "s"(w[1]), "s"(w[2]), "s"(w[3]));
     double ys[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        // high word ^= record & 0x80000000 in one VALU, no SALU mask (C3 kernel 0.600 -> 0.593 ms):
-        // bitop3 0x78 = a ^ (b & c), truth-table index 4a + 2b + c (the compiler's own form of
-        // y ^ (m & s)); sgn is the mask in a VGPR
-        const uint64_t yb = __builtin_bit_cast(uint64_t, y[q]);
-        uint32_t hi;
-        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x78" : "=v"(hi) : "v"((uint32_t)(yb >> 32)), "v"(sgn), "s"(w[q]));
-        ys[q] = __builtin_bit_cast(double, (yb & 0xffffffffull) | ((uint64_t)hi << 32));
-    }
+    for (int q = 0; q < 4; ++q) ys[q] = __builtin_bit_cast(double, (yb[q] & 0xffffffffull) | ((uint64_t)hi[q] << 32));
     asm volatile("s_set_gpr_idx_on %7, gpr_idx(SRC0,DST)\n\t"
                  "s_lshr_b32 %3, %15, 8\n\t"
                  "v_add_f64 v[32:33], v[32:33], %11\n\t"
