@@ -6,9 +6,12 @@ inside the fused MFMA GEMM, A ~ DenseDist(m, n) Gaussian key 99 ColMajor (genera
 resident in HBM before timing), d = 1024, m = n = 16384, alpha = 1, beta = 0.
 
 A "step" is one sketch_general call over the whole A. With N > 1 ranks (torchrun, RCCL) the job is
-weak-scaled by output rows: rank g computes rows [g*d, (g+1)*d) of the (N*d) x n sketch of the
-operator DenseDist(N*d, m) (ro_s = g*d, the reference's reproducible-submatrix property) and an
-RCCL all-gather reassembles the full ColMajor sketch on every rank inside the timed step.
+sharded by output rows (ro_s, the reference's reproducible-submatrix property) and an RCCL
+all-gather reassembles the full ColMajor sketch on every rank inside the timed step:
+  * default, weak scaling: rank g computes rows [g*d, (g+1)*d) of the (N*d) x n sketch of the
+    operator DenseDist(N*d, m);
+  * --split-d, strong scaling (a fixed problem): the config's total d (D_TOTAL; configs[3] and the
+    north star: d = 2048) is split, rank g computing rows [g*d/N, (g+1)*d/N).
 
 SASO (c3) shards by columns instead: rank g owns columns [g*n, (g+1)*n) of an
 m x (N*n) A -- it reads only those -- samples the same operator, and the all-gather of the
@@ -17,7 +20,7 @@ contiguous ColMajor column blocks reassembles the d x (N*n) sketch.
 `--gpus N` with N > 1 outside torchrun relaunches itself under `torch.distributed.run` (one rank per
 GPU, 127.0.0.1 rendezvous) before anything touches the GPU; under torchrun WORLD_SIZE must equal N.
 
-Prints ONE JSON line (rank 0). value = N*d*n / t_step (entries/s, whole job); roofline = the fused
+Prints ONE JSON line (rank 0). value = d_total*n / t_step (entries/s, whole job); roofline = the fused
 GEMM kernel's algorithmic flops (2*d*m*n per launch) / its average launch time measured with HIP
 events on the launch stream; cpu_baseline = the oracle's OpenMP fill + host BLAS dgemm (the
 reference's algorithm, oracle/) on a bounded column sample, rank 0 only.
@@ -42,6 +45,10 @@ import randblas_amd as rb  # noqa: E402
 
 PEAK = {"f64": 78.6e12, "f32": 157.3e12}   # MI355X dense matrix peaks (MI355X_MICROARCH.md)
 HBM_PEAK = 8.0e12
+
+# --split-d (fixed problem, strong scaling): the TOTAL operator rows, split over the ranks. c4's
+# weak-scaled d = 256 per GPU is configs[3]'s d = 2048 over 8 GPUs; the others are their own total.
+D_TOTAL = {"c1": 128, "c2": 1024, "ns": 2048, "c4": 2048, "c5": 512, "c5p": 512}
 
 CONFIGS = {
     # name: (kind, dtype, d, m, n, vec_nnz)
@@ -86,6 +93,19 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def cpu_model():
+    """The host CPU's model name (/proc/cpuinfo), for the baseline's record."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(kind, dtype, d, m, n, vec_nnz, target_s=10.0):
     """The oracle (reference algorithm restated in C + host BLAS) on a bounded sample of columns."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -121,6 +141,8 @@ def cpu_baseline(kind, dtype, d, m, n, vec_nnz, target_s=10.0):
         "value": d * ns / tmed,
         "unit": "sketched entries/s",
         "cores": cores,
+        "cpu": cpu_model(),
+        "nproc": os.cpu_count(),
         "kind": "port",
         "sample": f"{kind} {dtype} d={d} m={m} on {ns} of the {n} columns of A, median of {reps} "
                   f"(OpenMP Philox/Box-Muller fill + {os.path.basename(O.BLAS)} gemm)" if kind != "saso" else
@@ -147,9 +169,25 @@ def relaunch(ngpus: int) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+def shard_rows(args, world):
+    """(d_total, d_per_gpu, scaling) of a dense config: weak scaling keeps d rows per GPU (the job
+    is the (world d) x n sketch); --split-d keeps the problem (D_TOTAL rows) and gives each rank
+    D_TOTAL / world of them."""
+    kind, _, d, _, _, _ = CONFIGS[args.config]
+    if not args.split_d:
+        return (d if kind == "saso" else world * d), d, "weak"
+    if kind == "saso":
+        raise SystemExit("bench: --split-d applies to the dense configs (SASO shards by columns)")
+    total = D_TOTAL[args.config]
+    if total % world:
+        raise SystemExit(f"bench: --split-d needs d = {total} divisible by the {world} ranks")
+    return total, total // world, "strong"
+
+
 def dry_run(args, world, rank):
     """--dry-run: the launch / rendezvous / reporting path without device work (CPU, gloo):
     every rank joins, the max-over-ranks reduction runs, rank 0 prints the line's skeleton."""
+    d_total, d_loc, scaling = shard_rows(args, world)
     if world > 1:
         dist.init_process_group("gloo")
     t = torch.tensor([float(rank)], dtype=torch.float64)
@@ -157,7 +195,8 @@ def dry_run(args, world, rank):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     if rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_max": float(t.item()), "config": args.config,
-                          "steps": args.steps, "warmup": args.warmup}), flush=True)
+                          "steps": args.steps, "warmup": args.warmup, "d": d_total, "d_per_gpu": d_loc,
+                          "ro_s": [g * d_loc for g in range(world)], "scaling": scaling}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -172,6 +211,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--chunks", type=int, default=4, help="column chunks pipelined with the all-gather (N > 1)")
     ap.add_argument("--dry-run", action="store_true", help="launch/report path only, no device work (CPU, gloo)")
+    ap.add_argument("--lda-pad", type=int, default=0,
+                    help="diagnostics: store the dense A with leading dimension m + pad (same matrix)")
+    ap.add_argument("--split-d", action="store_true",
+                    help="fixed problem (strong scaling): the config's total d split over the ranks (ro_s = g d / N)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -192,6 +235,7 @@ def main():
     torch.cuda.set_device(dev)
 
     kind, dtype, d, m, n, vec_nnz = CONFIGS[args.config]
+    d_total, d, scaling = shard_rows(args, world)   # d: this rank's rows (dense) / all rows (SASO)
     tdt = torch.float64 if dtype == "f64" else torch.float32
     stream = torch.cuda.current_stream(dev)
 
@@ -203,7 +247,13 @@ def main():
         S = rb.SparseSkOp(rb.SparseDist(d, m, vec_nnz), rb.RNGState(0))
     else:
         rb.fill_dense("C", rb.DenseDist(m, n), m, n, 0, 0, A, rb.RNGState(99))
-        S = rb.DenseSkOp(rb.DenseDist(world * d, m), rb.RNGState(0))
+        S = rb.DenseSkOp(rb.DenseDist(d_total, m), rb.RNGState(0))
+    lda = m + args.lda_pad
+    if args.lda_pad and kind == "dense":
+        Ap = torch.empty(lda * n, dtype=tdt, device=dev)
+        Ap.view(n, lda)[:, :m].copy_(A.view(n, m))
+        A = Ap
+        del Ap
     if kind in ("sksy", "sksyp"):   # A symmetric: A := (A + A^T) / 2 (input prep, not timed)
         Am = A.view(n, m)
         A.copy_(((Am + Am.t()) * 0.5).reshape(-1))
@@ -230,14 +280,13 @@ def main():
     def compute(ro_s, j0, j1, out, record=False):
         """This rank's shard of B = S A over columns j0 .. j1 of its A: rows ro_s .. ro_s + d (dense),
         all d rows (SASO, whose A block is already this rank's columns)."""
-        Ach = A[j0 * m:]
-        timed(lambda: rb.sketch_general_left("C", "N", "N", d, j1 - j0, m, 1.0, S, Ach, m, 0.0, out, d, ro_s=ro_s),
+        Ach = A[j0 * lda:]
+        timed(lambda: rb.sketch_general_left("C", "N", "N", d, j1 - j0, m, 1.0, S, Ach, lda, 0.0, out, d, ro_s=ro_s),
               record)
 
     def sksy(ro_s, out, record=False):
         """One sketch_symmetric call (sksy.hh:520-537) with the reference's default sym_check_tol = 0:
-        the device symmetry check, then the sketch, which reads only A's upper triangle once the
-        check has found A bitwise symmetric."""
+        the device symmetry check, then the sketch on A's full storage (as the reference computes it)."""
         timed(lambda: rb.sketch_symmetric_left("C", d, n, 1.0, S, A, n, 0.0, out, d, ro_s=ro_s, sym_check_tol=0.0),
               record)
 
@@ -259,13 +308,13 @@ def main():
     elif world > 1:
         from randblas_amd.distributed import RowShardedSketch
 
-        B_full = torch.empty(world * d * n, dtype=tdt, device=dev)
+        B_full = torch.empty(d_total * n, dtype=tdt, device=dev)
         if kind in ("sksy", "sksyp"):   # the symmetric sketch takes the whole square A: one chunk per rank
             fn = sksy if kind == "sksy" else sksyp
-            drv = RowShardedSketch(world * d, n, lambda ro, j0, j1, out: fn(ro, out, recording[0]), tdt, dev,
+            drv = RowShardedSketch(d_total, n, lambda ro, j0, j1, out: fn(ro, out, recording[0]), tdt, dev,
                                    chunks=1)
         else:
-            drv = RowShardedSketch(world * d, n, lambda ro, j0, j1, out: compute(ro, j0, j1, out, recording[0]),
+            drv = RowShardedSketch(d_total, n, lambda ro, j0, j1, out: compute(ro, j0, j1, out, recording[0]),
                                    tdt, dev, chunks=args.chunks)
 
         def step(record=False):
@@ -335,7 +384,8 @@ def main():
     if rank == 0:
         line = {
             "metric": "sketched-entries/sec (d*n/s) + achieved-%-of-fp64-MFMA-peak, skge d x m * m x n",
-            "value": world * d * n / (ms_step * 1e-3),   # d x (world n) entries for SASO, (world d) x n dense
+            # d x (world n) entries for SASO, d_total x n dense
+            "value": (world * d * n if kind == "saso" else d_total * n) / (ms_step * 1e-3),
             "unit": "sketched entries/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -345,7 +395,7 @@ def main():
             "kernel_launches_per_step": launches / args.steps,
             "library_ms_per_step": call_ms,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": dtype,
             "data": ("synthetic (A ~ Gaussian DenseDist(m,n) key 99 generated on device; "
@@ -358,7 +408,7 @@ def main():
                                     "c4": "Gaussian skge fp32 (configs[3])",
                                     "c5": "sksy fp64, sketch_symmetric with sym_check_tol=0 (configs[4])",
                                     "c5p": "sksy fp64 on packed-symmetric A (configs[4] as worded)"}[args.config],
-                       "d": d if kind == "saso" else world * d, "d_per_gpu": d, "m": m,
+                       "d": d if kind == "saso" else d_total, "d_per_gpu": d, "m": m,
                        "n": world * n if kind == "saso" else n, "n_per_gpu": n, "layout": "ColMajor",
                        "operator": "SparseSkOp SASO" if kind == "saso" else "DenseSkOp Gaussian MajorAxis::Long",
                        "symmetry_check": ("tol=0, timed in the step" if kind == "sksy" else None),

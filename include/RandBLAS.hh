@@ -9,14 +9,16 @@
 //   sketch_vector x2 (skve.hh:152-258), sparse_data::{COO,CSR,CSC}Matrix views
 //   (sparse_data/{coo,csr,csc}_matrix.hh, int64 zero-based indices) and sketch_sparse x2
 //   (sparse_data/sksp.hh:464-615),
+//   dense::lskge3 / rskge3 and sparse::lskges / rskges (skge.hh:173-641), sparse::nnz /
+//   coo_view_of_skop (sparse_skops.hh:465-490), submatrix_as_blackbox (dense_skops.hh:594-602),
 //   exceptions::Error (exceptions.hh:45-70), and the blas::Layout / blas::Op enums of BLAS++,
 // and routes every call to the MI355X C ABI (include/randblas_hip.h). Host arrays work as in
 // the reference (they are staged through HBM; the call is synchronous); device arrays
 // (hipMalloc) are used in place. Link with -lrandblas_hip.
 //
-// Dense operators are never materialised: a DenseSkOp whose buff is nullptr is regenerated from
-// its Philox counters inside the fused MFMA GEMM. fill_dense(S) still fills S.buff (host memory,
-// as in the reference), after which the operator is applied from that buffer.
+// A DenseSkOp whose buff is nullptr is regenerated from its Philox counters inside the fused MFMA
+// GEMM, tile by tile into LDS; it is not written to memory. fill_dense(S) and submatrix_as_blackbox
+// still fill a host buffer, as in the reference, after which the operator is applied from it.
 #pragma once
 
 #include <algorithm>
@@ -221,6 +223,16 @@ struct DenseSkOp {
         RBH_CXX_REQUIRE(this->dist.n_cols > 0);
         if (dist.family == DenseDistName::BlackBox) RBH_CXX_REQUIRE(this->buff != nullptr);
     }
+    // A copy views the same buffer without owning it; a move takes the ownership along (the
+    // reference's implicit copy would delete an owned buffer twice).
+    DenseSkOp(const DenseSkOp &o)
+        : n_rows(o.n_rows), n_cols(o.n_cols), dist(o.dist), seed_state(o.seed_state), next_state(o.next_state),
+          buff(o.buff), layout(o.layout), del_buff_on_destruct(false) {}
+    DenseSkOp(DenseSkOp &&o) noexcept
+        : n_rows(o.n_rows), n_cols(o.n_cols), dist(o.dist), seed_state(o.seed_state), next_state(o.next_state),
+          buff(o.buff), layout(o.layout), del_buff_on_destruct(o.del_buff_on_destruct) {
+        o.del_buff_on_destruct = false;
+    }
     ~DenseSkOp() {
         if (del_buff_on_destruct) delete[] buff;
     }
@@ -285,6 +297,25 @@ void fill_dense(DenseSkOpT &S) {
     S.buff = new T[S.dist.n_rows * S.dist.n_cols];
     fill_dense(S.dist, S.buff, S.seed_state);
     S.del_buff_on_destruct = true;
+}
+
+// submatrix_as_blackbox (dense_skops.hh:594-602): the n_rows x n_cols window of S at (ro_s, co_s),
+// filled (on the device, copied to a host buffer the result owns) in S's natural layout, as a
+// BlackBox operator. (dense::lskge3 / rskge3 never call it: they regenerate the window inside the
+// GEMM instead.)
+template <typename T, typename RNG>
+DenseSkOp<T, RNG> submatrix_as_blackbox(const DenseSkOp<T, RNG> &S, int64_t n_rows, int64_t n_cols, int64_t ro_s,
+                                        int64_t co_s) {
+    T *buff = new T[n_rows * n_cols];
+    const blas::Layout dl = dist_to_layout(S.dist);
+    try {
+        fill_dense(dl, S.dist, n_rows, n_cols, ro_s, co_s, buff, S.seed_state);
+    } catch (...) {
+        delete[] buff;
+        throw;
+    }
+    DenseDist submatrix_dist(n_rows, n_cols, DenseDistName::BlackBox, MajorAxis::Undefined);
+    return DenseSkOp<T, RNG>(n_rows, n_cols, submatrix_dist, S.seed_state, S.next_state, buff, dl, true);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -477,6 +508,47 @@ void rsk(blas::Layout layout, blas::Op opA, blas::Op opS, int64_t m, int64_t d, 
 }
 }  // namespace detail
 
+// The layer under sketch_general that the reference's own test harness calls by name
+// (test/test_matmul_cores/linop_common.hh:155,171,485,500).
+namespace dense {
+// dense::lskge3 (skge.hh:173-215): B = alpha op(submat(S)) op(A) + beta B
+template <typename T, typename RNG>
+void lskge3(blas::Layout layout, blas::Op opS, blas::Op opA, int64_t d, int64_t n, int64_t m, T alpha,
+            DenseSkOp<T, RNG> &S, int64_t ro_s, int64_t co_s, const T *A, int64_t lda, T beta, T *B, int64_t ldb) {
+    detail::lsk(layout, opS, opA, d, n, m, alpha, S, ro_s, co_s, A, lda, beta, B, ldb);
+}
+// dense::rskge3 (skge.hh:320-364): B = alpha op(A) op(submat(S)) + beta B
+template <typename T, typename RNG>
+void rskge3(blas::Layout layout, blas::Op opA, blas::Op opS, int64_t m, int64_t d, int64_t n, T alpha, const T *A,
+            int64_t lda, DenseSkOp<T, RNG> &S, int64_t ro_s, int64_t co_s, T beta, T *B, int64_t ldb) {
+    detail::rsk(layout, opA, opS, m, d, n, alpha, A, lda, S, ro_s, co_s, beta, B, ldb);
+}
+}  // namespace dense
+
+namespace sparse {
+// sparse::lskges (skge.hh:485-510): fills S if needed, then left_spmm of its COO view
+template <typename T, typename SKOP>
+inline void lskges(blas::Layout layout, blas::Op opS, blas::Op opA, int64_t d, int64_t n, int64_t m, T alpha, SKOP &S,
+                   int64_t ro_s, int64_t co_s, const T *A, int64_t lda, T beta, T *B, int64_t ldb) {
+    detail::lsk(layout, opS, opA, d, n, m, alpha, S, ro_s, co_s, A, lda, beta, B, ldb);
+}
+// sparse::rskges (skge.hh:616-641): fills S if needed, then right_spmm of its COO view
+template <typename T, typename SKOP>
+inline void rskges(blas::Layout layout, blas::Op opA, blas::Op opS, int64_t m, int64_t d, int64_t n, T alpha,
+                   const T *A, int64_t lda, SKOP &S, int64_t ro_s, int64_t co_s, T beta, T *B, int64_t ldb) {
+    detail::rsk(layout, opA, opS, m, d, n, alpha, A, lda, S, ro_s, co_s, beta, B, ldb);
+}
+// sparse::nnz (sparse_skops.hh:465-481): the entries a SparseSkOp of this dist holds
+template <typename SKOP>
+inline int64_t nnz(SKOP const &S0) {
+    const bool saso = S0.dist.major_axis == MajorAxis::Short, wide = S0.dist.n_rows < S0.dist.n_cols;
+    if (saso && wide) return S0.dist.vec_nnz * S0.dist.n_cols;
+    if (saso) return S0.dist.vec_nnz * S0.dist.n_rows;
+    if (wide) return S0.dist.vec_nnz * S0.dist.n_rows;
+    return S0.dist.vec_nnz * S0.dist.n_cols;   // tall LASO
+}
+}  // namespace sparse
+
 // Left, submatrix: B = alpha op(submat(S)) op(A) + beta B
 template <typename T, typename SKOP>
 inline void sketch_general(blas::Layout layout, blas::Op opS, blas::Op opA, int64_t d, int64_t n, int64_t m, T alpha,
@@ -644,6 +716,11 @@ struct COOMatrix {
     }
     ~COOMatrix() { if (own_memory) { delete[] vals; delete[] rows; delete[] cols; } }
     COOMatrix(const COOMatrix &) = delete;
+    COOMatrix(COOMatrix &&o) noexcept
+        : n_rows(o.n_rows), n_cols(o.n_cols), own_memory(o.own_memory), nnz(o.nnz), index_base(o.index_base),
+          vals(o.vals), rows(o.rows), cols(o.cols), sort(o.sort) {
+        if (o.own_memory) o.vals = nullptr, o.rows = nullptr, o.cols = nullptr;
+    }
     static constexpr char fmt = 'O';
     const sint_t *ptr_arr() const { return rows; }
     const sint_t *idx_arr() const { return cols; }
@@ -702,6 +779,16 @@ struct CSCMatrix {
 using sparse_data::COOMatrix;
 using sparse_data::CSCMatrix;
 using sparse_data::CSRMatrix;
+
+namespace sparse {
+// sparse::coo_view_of_skop (sparse_skops.hh:483-490): a non-owning COOMatrix over S's arrays,
+// filling S first if it is not yet filled
+template <typename SkOp, typename T = typename SkOp::scalar_t, typename sint_t = typename SkOp::index_t>
+COOMatrix<T, sint_t> coo_view_of_skop(SkOp &S) {
+    if (!S.known_filled) fill_sparse(S);
+    return COOMatrix<T, sint_t>(S.dist.n_rows, S.dist.n_cols, nnz(S), S.vals, S.rows, S.cols);
+}
+}  // namespace sparse
 
 namespace detail {
 template <typename SpMat, typename = void> struct is_spmat : std::false_type {};

@@ -21,7 +21,7 @@ __global__ void fill_dense_kernel(const GenOperand g, int64_t n_rows_, int64_t n
         const int64_t q = qa + (c - r * nq);
         uint32_t ctr[4];
         rb::ctr_add(g.ctr, (uint64_t)(g.pr0 + r) * g.stride + (uint64_t)q, ctr);
-        const rb::u32x4 w = rb::philox4x32<10>(ctr[0], ctr[1], ctr[2], ctr[3], g.key[0], g.key[1]);
+        const rb::u32x4 w = rb::philox4x32_uk<10>(ctr[0], ctr[1], ctr[2], ctr[3], g.key[0], g.key[1]);
         float s[4];
         rb::sample4<FAMILY>(w, s);
 #pragma unroll

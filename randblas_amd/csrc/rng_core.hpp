@@ -69,6 +69,39 @@ RB_HD u32x4 philox4x32(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint3
     return out;
 }
 
+#if defined(__HIPCC__)
+// a ^ b ^ k in one v_bitop3_b32 (gfx950 has no v_xor3) with the key word k in an SGPR. For
+// wave-uniform k only: every Philox key of the library comes from a kernel argument.
+__device__ __forceinline__ uint32_t xor3_uk(uint32_t a, uint32_t b, uint32_t k) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
+}
+#endif
+
+// philox4x32 with a wave-uniform key: the same words, the round's two three-way xors as one
+// instruction each on the device (the dense draws, where every Philox call is on the critical
+// issue path beside the MFMAs).
+template <int R = 10>
+RB_HD u32x4 philox4x32_uk(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (r > 0) { k0 += PHILOX_W0; k1 += PHILOX_W1; }
+        uint32_t hi0, lo0, hi1, lo1;
+        mulhilo32(PHILOX_M0, c0, hi0, lo0);
+        mulhilo32(PHILOX_M1, c2, hi1, lo1);
+        const uint32_t n0 = xor3_uk(hi1, c1, k0);
+        const uint32_t n2 = xor3_uk(hi0, c3, k1);
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    }
+    u32x4 out = {{c0, c1, c2, c3}};
+    return out;
+#else
+    return philox4x32<R>(c0, c1, c2, c3, k0, k1);
+#endif
+}
+
 // 128-bit counter = base (4 x u32, little-endian words) + off (u64), carries across words.
 RB_HD void ctr_add(const uint32_t base[4], uint64_t off, uint32_t out[4]) {
     uint64_t lo = (uint64_t)base[0] + (uint32_t)off;
@@ -123,10 +156,12 @@ constexpr double SC_S1 = -0x1.555545995a603p-3;
 constexpr double SC_S2 =  0x1.1107605230bc4p-7;
 constexpr double SC_S3 = -0x1.994eb3774cf24p-13;
 
-// sin(y), cos(y) for |y| < 120 (the Box-Muller argument satisfies |y| < pi). The small-argument
+// sin(y), cos(y) for the Box-Muller arguments y = pi_f * uneg11(w), |y| < pi. The small-argument
 // branch of glibc (|y| < pi/4, no reduction) is the n == 0 case of the reduced path bit for bit
 // (n == 0 makes the reduction x - 0*hpi == x and the sign factor 1), so one branch-free path
-// serves both; the tiny branch (|y| < 2^-12) is kept as a select.
+// serves both. glibc's tiny branch (|y| < 2^-12: sin = y, cos = 1) needs no select either: there the
+// polynomial rounds to y and to 1 (x^2 / 6 and x^2 / 2 are below a quarter ulp). Both facts are
+// checked against glibc for all 2^32 words w (tools/check_glibc_math.cc).
 RB_HD void rb_sincosf(float y, float &sin_out, float &cos_out) {
 #if defined(__clang__)
 #pragma clang fp contract(off)
@@ -151,15 +186,12 @@ RB_HD void rb_sincosf(float y, float &sin_out, float &cos_out) {
     const float ps = (float)RB_FMA(x5, ss1, s);
     const float pc0 = (float)RB_FMA(x6, cc2, c);
     const float pc = (n & 2) ? -pc0 : pc0;
-    float so = (n & 1) ? pc : ps;
-    float co = (n & 1) ? ps : pc;
-    // |y| < 2^-12: sin = y, cos = 1
-    const bool tiny = ((f32_bits(y) >> 20) & 0x7ff) < ((f32_bits(0x1p-12f) >> 20) & 0x7ff);
-    sin_out = tiny ? y : so;
-    cos_out = tiny ? 1.0f : co;
+    sin_out = (n & 1) ? pc : ps;
+    cos_out = (n & 1) ? ps : pc;
 }
 
-// logf for normal positive finite x (the Box-Muller radius argument is u01 in [2^-33, 1]).
+// logf for normal positive finite x (the Box-Muller radius argument is u01 in [2^-33, 1]; all 2^32
+// of them are checked against glibc by tools/check_glibc_math.cc).
 constexpr double LOGF_LN2 = 0x1.62e42fefa39efp-1;
 constexpr double LOGF_A0 = -0x1.00ea348b88334p-2;
 constexpr double LOGF_A1 =  0x1.5575b0be00b6ap-2;
@@ -201,15 +233,17 @@ RB_HD float rb_logf_tab(float xf, const LogfEntry *tab) {
     double y = RB_FMA(LOGF_A1, r, LOGF_A2);
     y = RB_FMA(LOGF_A0, r2, y);
     y = RB_FMA(y, r2, y0 + r);
-    const float res = (float)y;
-    return (ix == 0x3f800000u) ? 0.0f : res;
+    return (float)y;   // (x = 1 needs no special case: table entry 9 is {1, 0}, so r = 0 and y = 0)
 }
 RB_HD float rb_logf(float xf) { return rb_logf_tab(xf, LOGF_TAB); }
 
-// Correctly rounded float sqrt via double (double rounding is innocuous for sqrt at p = 53).
+// Correctly rounded float sqrt. Host: via double (double rounding is innocuous for sqrt at
+// p = 53). Device: the compiler's correctly rounded f32 sqrt (HIP's default
+// -fhip-fp32-correctly-rounded-divide-sqrt: v_sqrt_f32 and an fma residual fix-up, about half the
+// issue cycles of the f64 sequence) -- the same bits, as any two correctly rounded results are.
 RB_HD float rb_sqrtf(float v) {
-#if defined(__HIPCC__)
-    return (float)__builtin_sqrt((double)v);
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_sqrtf(v);
 #else
     return (float)sqrt((double)v);
 #endif

@@ -67,7 +67,7 @@ __device__ __forceinline__ void gen_call(const GenOperand &g, uint64_t off, T ou
                                          const rb::LogfEntry *tab = rb::LOGF_TAB) {
     uint32_t c[4];
     rb::ctr_add(g.ctr, off, c);
-    const rb::u32x4 w = rb::philox4x32<10>(c[0], c[1], c[2], c[3], g.key[0], g.key[1]);
+    const rb::u32x4 w = rb::philox4x32_uk<10>(c[0], c[1], c[2], c[3], g.key[0], g.key[1]);
     float s[4];
     rb::sample4<FAMILY>(w, s, tab);
     if (FAMILY == rb::UNIFORM) {
@@ -703,7 +703,7 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
             }
             rb::ctr_add(gop.ctr, off, c);
         }
-        const rb::u32x4 w = rb::philox4x32<10>(c[0], c[1], c[2], c[3], gop.key[0], gop.key[1]);
+        const rb::u32x4 w = rb::philox4x32_uk<10>(c[0], c[1], c[2], c[3], gop.key[0], gop.key[1]);
         float sm[4];
         rb::sample4<FAMILY>(w, sm, tab);
 #pragma unroll
@@ -941,7 +941,7 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
             }
             rb::ctr_add(gop.ctr, off, c);
         }
-        const rb::u32x4 w = rb::philox4x32<10>(c[0], c[1], c[2], c[3], gop.key[0], gop.key[1]);
+        const rb::u32x4 w = rb::philox4x32_uk<10>(c[0], c[1], c[2], c[3], gop.key[0], gop.key[1]);
         float sm[4];
         rb::sample4<FAMILY>(w, sm, tab);
 #pragma unroll
@@ -1193,17 +1193,21 @@ static bool fused_ok(const GemmProblem &p) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Materialised generated operand (the reference's own order: fill_dense of submat(S), then GEMM)
+// Materialised generated operand (opt-in: RBH_MATERIALISE=1)
 // ------------------------------------------------------------------------------------------
-// A wide kernel that draws its operator tile regenerates every entry once per 512-row tile of the
-// memory operand: n / 512 = 32 times at C2, 64 at C4. When that factor reaches MAT_MIN_TILES the
-// launcher draws the window once into a workspace, gmat[o * K + k] (one Philox call per 4 entries,
-// the same samples as the in-kernel draw), and the wide kernel loads its tile from there (GMAT)
-// instead of drawing it. The LDS image and the MFMA order are unchanged, so the results are
-// bitwise those of the drawing kernel. Measured (C2 with the draw removed: 8.98 -> 8.41 ms) before
-// building it; RBH_NO_MAT=1 keeps the in-kernel draw.
+// By default the wide kernels draw their operator tile inside the GEMM, so the operator is never
+// written to memory (the north star). A drawing wide kernel regenerates every entry once per
+// 512-row tile of the memory operand (n / 512 = 32 times at C2), and on gfx950 an f64 / f32-input
+// MFMA holds its SIMD's issue for its whole duration (tools/micro/mfma_coexec.hip), so that draw's
+// VALU work adds to the MFMA time instead of hiding under it. With RBH_MATERIALISE=1 the launcher
+// instead does what the reference does (fill_dense of submat(S), then GEMM, skge.hh:173-215):
+// gen_fill_kernel draws the window once into a workspace, gmat[o * K + k], and the wide kernel
+// loads its tile from there (GMAT). The LDS image and the MFMA order are unchanged, so the results
+// are bitwise those of the drawing kernel. It applies when the memory operand spans at least
+// MAT_MIN_TILES wide tiles and the window fits MAT_MAX_BYTES; when the workspace cannot be
+// allocated the kernel draws in place instead.
 constexpr int64_t MAT_MIN_TILES = 4;
-constexpr int64_t MAT_MAX_BYTES = (int64_t)8 << 30;
+constexpr int64_t MAT_MAX_BYTES = (int64_t)2 << 30;
 
 template <typename T, int GK, int FAMILY>
 __global__ __launch_bounds__(256) void gen_fill_kernel(const GenOperand g, int64_t gnO, int64_t K, T *buf) {
@@ -1216,7 +1220,7 @@ __global__ __launch_bounds__(256) void gen_fill_kernel(const GenOperand g, int64
         const int64_t a = c / per, q = c - a * per;
         uint32_t cc[4];
         rb::ctr_add(g.ctr, (uint64_t)(g.pr0 + a) * g.stride + (uint64_t)(g.pc0 >> 2) + (uint64_t)q, cc);
-        const rb::u32x4 w = rb::philox4x32<10>(cc[0], cc[1], cc[2], cc[3], g.key[0], g.key[1]);
+        const rb::u32x4 w = rb::philox4x32_uk<10>(cc[0], cc[1], cc[2], cc[3], g.key[0], g.key[1]);
         float sm[4];
         rb::sample4<FAMILY>(w, sm);
         v4_t v;
@@ -1233,16 +1237,21 @@ __global__ __launch_bounds__(256) void gen_fill_kernel(const GenOperand g, int64
 }
 
 // the generated operand of p (GX: X) drawn into a workspace; *buf stays null when the kernel
-// should draw in place (few memory tiles, too large, or RBH_NO_MAT=1)
+// draws in place (the default; few memory tiles, too large, or no workspace)
 template <typename T, int GK, int FAMILY, bool GX>
 static hipError_t materialise(const GemmProblem &p, void **buf, hipStream_t s) {
-    static const bool off = [] { const char *e = getenv("RBH_NO_MAT"); return e && e[0] == '1'; }();
+    const char *env = getenv("RBH_MATERIALISE");   // read per call (a caller may switch it)
+    const bool on = env && env[0] == '1';
     *buf = nullptr;
     const int64_t gnO = GX ? p.M : p.N, mnO = GX ? p.N : p.M;
     const int64_t bytes = gnO * p.K * (int64_t)sizeof(T);
-    if (off || (mnO + 511) / 512 < MAT_MIN_TILES || bytes > MAT_MAX_BYTES || bytes <= 0) return hipSuccess;
+    if (!on || (mnO + 511) / 512 < MAT_MIN_TILES || bytes > MAT_MAX_BYTES || bytes <= 0) return hipSuccess;
     hipError_t e = ws_alloc(buf, (size_t)bytes, s);
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess) {   // no room: draw in place
+        (void)hipGetLastError();
+        *buf = nullptr;
+        return hipSuccess;
+    }
     const GenOperand &g = GX ? p.xg : p.yg;
     const int64_t calls = (GK == GEN_OK ? gnO * (p.K / 4) : p.K * ((gnO + 3) / 4));
     int64_t blocks = (calls + 255) / 256;
@@ -1268,16 +1277,6 @@ static hipError_t launch_wide(const GemmProblem &p, hipStream_t s) {
     e = materialise<T, GK, FAMILY, GX>(p, &gm, s);
     if (e != hipSuccess) return e;
     q.gmat = gm;
-#ifdef RBH_MAT_GENERIC
-    if (gm && TRI == 0 && split == 1) {   // experiment: the 128 x 256 generic kernel on two memory operands
-        GemmProblem r = p;
-        MemOperand m{gm, p.K, 1};
-        if (GX) { r.xkind = MEM; r.xm = m; r.xmode = 2; } else { r.ykind = MEM; r.ym = m; r.ymode = 2; }
-        e = launch_one<T, MEM, MEM, rb::GAUSSIAN, 128, 256, 2, 4>(r, s);
-        const hipError_t e2 = ws_free(gm, s);
-        return e != hipSuccess ? e : e2;
-    }
-#endif
     if (split > 1) {
         e = ws_alloc(&q.partial, sizeof(T) * (size_t)split * p.M * p.N, s);
         if (e != hipSuccess) { if (gm) (void)ws_free(gm, s); return e; }
@@ -1398,6 +1397,8 @@ static hipError_t launch_gemm_tri(const GemmProblem &p, hipStream_t s) {
     const MemOperand &m = gx ? p.ym : p.xm;
     if ((gx ? p.xkind : p.ykind) != GEN_OK || (g.pc0 & 3) || p.K % BK) return hipErrorNotSupported;
     if (p.tri <= 2 && ((((uintptr_t)m.ptr) % 16) || (m.so & 1))) return hipErrorNotSupported;
+    // tiles inside the triangle take the plain 32-bit byte-offset loads
+    if (p.tri <= 2 && !wide_offsets_ok<double>(p)) return hipErrorNotSupported;
     // 31-bit element indices in the kernel
     const int64_t n = p.tri_n, last = p.tri <= 2 ? (n - 1) * m.so + n : n * (n + 1) / 2;
     if (last >= ((int64_t)1 << 31)) return hipErrorNotSupported;

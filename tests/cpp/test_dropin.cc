@@ -425,6 +425,91 @@ static void symmetric_one_triangle() {
     }
 }
 
+// The layer under sketch_general, called by name exactly as the reference's own harness calls it:
+// RandBLAS::dense::lskge3 / rskge3 and RandBLAS::sparse::lskges / rskges
+// (test/test_matmul_cores/linop_common.hh:155,171,485,500), sparse::coo_view_of_skop (:110) and
+// sparse::nnz (test/test_datastructures/test_spmats/test_coo.cc:55,145-149), submatrix_as_blackbox
+// (dense_skops.hh:594-602, the window skge.hh:192-196 materialises).
+static void namespaced_entry_points() {
+    const int64_t d = 19, m = 201, n = 12;
+    auto A = random_matrix<double>(m, n, 99);
+    auto B0 = random_matrix<double>(d, n, 42);
+    const double eps = std::numeric_limits<double>::epsilon();
+    // dense::lskge3 on a 19 x 201 window at (2, 3) of a 24 x 210 operator == sketch_general's
+    RandBLAS::DenseSkOp<double> S(RandBLAS::DenseDist(24, 210), 7);
+    std::vector<double> B1(B0), B2(B0);
+    RandBLAS::dense::lskge3(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, m, 0.5, S, 2, 3, A.data(), m, -1.0,
+                            B1.data(), d);
+    RandBLAS::sketch_general(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, m, 0.5, S, 2, 3, A.data(), m, -1.0,
+                             B2.data(), d);
+    for (int64_t e = 0; e < d * n; ++e) CHECK(B1[e] == B2[e]);
+    // submatrix_as_blackbox: the same window as a BlackBox operator with its own host buffer
+    {
+        auto sub = RandBLAS::submatrix_as_blackbox(S, d, m, 2, 3);
+        CHECK(sub.dist.family == RandBLAS::DenseDistName::BlackBox);
+        CHECK(sub.del_buff_on_destruct && sub.buff != nullptr);
+        CHECK(sub.layout == Layout::RowMajor);   // dist_to_layout of the wide 24 x 210 Long-axis operator
+        std::vector<double> Se(24 * 210);
+        RandBLAS::fill_dense(Layout::RowMajor, S.dist, 24, 210, 0, 0, Se.data(), S.seed_state);
+        for (int64_t i = 0; i < d; ++i)
+            for (int64_t k = 0; k < m; ++k) CHECK(sub.buff[i * m + k] == Se[(2 + i) * 210 + 3 + k]);
+        // the materialised window applied through lskge3 == the fused window, within the bound
+        std::vector<double> B3(B0);
+        RandBLAS::dense::lskge3(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, m, 0.5, sub, 0, 0, A.data(), m, -1.0,
+                                B3.data(), d);
+        for (int64_t i = 0; i < d; ++i)
+            for (int64_t j = 0; j < n; ++j) {
+                double bound = std::fabs(B0[i + j * d]) * eps;
+                for (int64_t k = 0; k < m; ++k) bound += 0.5 * std::fabs(sub.buff[i * m + k] * A[k + j * m]) * m * 2 * eps;
+                CHECK(std::fabs(B3[i + j * d] - B1[i + j * d]) <= 2 * bound);
+            }
+    }
+    // dense::rskge3: B (n x d2) = A^T (n x m) S (m x d2)
+    const int64_t d2 = 7;
+    RandBLAS::DenseSkOp<double> R(RandBLAS::DenseDist(m, d2), 57);
+    std::vector<double> Br1(n * d2, 0.0), Br2(n * d2, 0.0);
+    RandBLAS::dense::rskge3(Layout::ColMajor, Op::Trans, Op::NoTrans, n, d2, m, 1.0, A.data(), m, R, 0, 0, 0.0,
+                            Br1.data(), n);
+    RandBLAS::sketch_general(Layout::ColMajor, Op::Trans, Op::NoTrans, n, d2, m, 1.0, A.data(), m, R, 0, 0, 0.0,
+                             Br2.data(), n);
+    for (int64_t e = 0; e < n * d2; ++e) CHECK(Br1[e] == Br2[e]);
+    // sparse::lskges / rskges: unfilled operators come back filled, same bits as sketch_general
+    RandBLAS::SparseDist DS{d, m, 3};
+    RandBLAS::SparseSkOp<double> L1(DS, 42), L2(DS, 42);
+    std::vector<double> Bs1(B0), Bs2(B0);
+    RandBLAS::sparse::lskges(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, m, 5.5, L1, 0, 0, A.data(), m, -1.0,
+                             Bs1.data(), d);
+    RandBLAS::sketch_general(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, m, 5.5, L2, 0, 0, A.data(), m, -1.0,
+                             Bs2.data(), d);
+    CHECK(L1.known_filled);
+    for (int64_t e = 0; e < d * n; ++e) CHECK(Bs1[e] == Bs2[e]);
+    RandBLAS::SparseSkOp<double> Rs1(RandBLAS::SparseDist{m, d, 2}, 3), Rs2(RandBLAS::SparseDist{m, d, 2}, 3);
+    std::vector<double> Bq1(n * d, 0.0), Bq2(n * d, 0.0);
+    RandBLAS::sparse::rskges(Layout::ColMajor, Op::Trans, Op::NoTrans, n, d, m, 1.0, A.data(), m, Rs1, 0, 0, 0.0,
+                             Bq1.data(), n);
+    RandBLAS::sketch_general(Layout::ColMajor, Op::Trans, Op::NoTrans, n, d, m, 1.0, A.data(), m, Rs2, 0, 0, 0.0,
+                             Bq2.data(), n);
+    for (int64_t e = 0; e < n * d; ++e) CHECK(Bq1[e] == Bq2[e]);
+    // sparse::coo_view_of_skop + sparse::nnz (test_coo.cc:55,145-149): fills an unfilled operator,
+    // and the view's dense image equals the operator's
+    for (RandBLAS::MajorAxis ma : {RandBLAS::MajorAxis::Short, RandBLAS::MajorAxis::Long}) {
+        RandBLAS::SparseSkOp<double> So(RandBLAS::SparseDist{d, m, 2, ma}, 1);
+        auto Acoo = RandBLAS::sparse::coo_view_of_skop(So);
+        CHECK(So.known_filled);
+        CHECK(Acoo.n_rows == So.dist.n_rows);
+        CHECK(Acoo.n_cols == So.dist.n_cols);
+        CHECK(RandBLAS::sparse::nnz(So) == Acoo.nnz);
+        CHECK(RandBLAS::sparse::nnz(So) == So.nnz_count());
+        CHECK(Acoo.rows == So.rows && Acoo.cols == So.cols && Acoo.vals == So.vals);
+        CHECK(!Acoo.own_memory);
+        std::vector<double> img(d * m, 0.0);
+        for (int64_t e = 0; e < Acoo.nnz; ++e) img[Acoo.rows[e] + Acoo.cols[e] * d] += Acoo.vals[e];
+        int64_t nz = 0;
+        for (double v : img) nz += v != 0.0;
+        CHECK(nz == RandBLAS::sparse::nnz(So));   // no duplicate (row, col) in a SASO / LASO
+    }
+}
+
 int main() {
 #ifdef ONLY_SKSP   // diagnostics: the sketch_sparse checks alone
     try {
@@ -448,6 +533,7 @@ int main() {
     sparse_operator_state();
     spmm_both_sides();
     symmetric_one_triangle();
+    namespaced_entry_points();
     if (g_fail) {
         std::printf("%d checks FAILED\n", g_fail);
         return 1;

@@ -266,19 +266,46 @@ def test_row_shards_reassemble(cuda):
     assert np.array_equal(np.vstack(parts), full)
 
 
-# Memory operands spanning >= 4 wide tiles (here 2100 outer indices) take the materialised-operator
-# kernels (skge_dense.hip: gen_fill_kernel + the GMAT wide kernels): generated rows not a multiple of
-# 64, a ragged last tile, a submatrix window, both families and major axes, f64 and f32 (K = 256 is a
-# multiple of both step depths), left and right sketches.
+# Memory operands spanning >= 4 wide tiles (here 2100 outer indices): the drawing wide kernels (the
+# default: the operator tile is regenerated in LDS and never stored) and, with RBH_MATERIALISE=1, the
+# opt-in materialised-operator kernels (gen_fill_kernel + the GMAT wide kernels). Generated rows not
+# a multiple of 64, a ragged last tile, a submatrix window, both families and major axes, f64 and
+# f32 (K = 256 is a multiple of both step depths), left and right sketches.
+@pytest.fixture(params=["draw", "materialise"])
+def operator_mode(request, monkeypatch):
+    if request.param == "materialise":
+        monkeypatch.setenv("RBH_MATERIALISE", "1")
+    else:
+        monkeypatch.delenv("RBH_MATERIALISE", raising=False)
+    return request.param
+
+
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("layout", ["C", "R"])
 @pytest.mark.parametrize("fam,maj", [("G", "L"), ("G", "S"), ("U", "L")])
-def test_lskge3_materialised(cuda, dtype, layout, fam, maj):
+def test_lskge3_wide_tiles(cuda, operator_mode, dtype, layout, fam, maj):
     check_left(cuda, layout, "N", "N", 100, 2100, 256, 1.5, 0.5, 120, 300, 8, 4, dtype, fam=fam, maj=maj)
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("layout", ["C", "R"])
 @pytest.mark.parametrize("fam,maj", [("G", "L"), ("U", "S")])
-def test_rskge3_materialised(cuda, dtype, layout, fam, maj):
+def test_rskge3_wide_tiles(cuda, operator_mode, dtype, layout, fam, maj):
     check_right(cuda, layout, "N", "N", 2100, 100, 256, -0.5, 0.0, 300, 120, 4, 8, dtype, fam=fam, maj=maj)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_materialised_equals_drawn_bitwise(cuda, monkeypatch, dtype):
+    """The opt-in materialised window feeds the wide kernel the same LDS image in the same MFMA
+    order as the in-kernel draw: bitwise the same sketch."""
+    d, n, m = 130, 2600, 512
+    A = dev(O.random_matrix(m, n, 99, dtype), cuda)
+    S = rb.DenseSkOp(rb.DenseDist(d + 6, m + 32), rb.RNGState(3))
+    out = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("RBH_MATERIALISE", mode)
+        B = torch.empty(d * n, dtype=A.dtype, device=cuda)
+        rb.sketch_general_left("C", "N", "N", d, n, m, dtype(1.0), S, A, m, dtype(0.0), B, d, ro_s=4, co_s=8)
+        out.append(host(B))
+    ut = np.uint64 if dtype == np.float64 else np.uint32
+    assert np.array_equal(out[0].view(ut), out[1].view(ut))

@@ -101,13 +101,9 @@ def sym_full(n, seed):
 
 def store(M, layout, lda):
     n = M.shape[0]
-    buf = np.zeros(lda * n)
-    for j in range(n):
-        if layout == "C":
-            buf[j * lda:j * lda + n] = M[:, j]
-        else:
-            buf[j * lda:j * lda + n] = M[j, :]
-    return buf
+    buf = np.zeros((n, lda), dtype=M.dtype)
+    buf[:, :n] = M.T if layout == "C" else M   # row j of buf = column j (ColMajor) / row j (RowMajor)
+    return buf.reshape(-1)
 
 
 def packed(M, layout, uplo):
@@ -132,16 +128,19 @@ def packed(M, layout, uplo):
 def poison_other_triangle(buf, n, lda, layout, uplo):
     """NaN in every stored slot of the triangle that is NOT uplo (the diagonal stays)."""
     out = buf.copy()
-    for j in range(n):
-        for i in range(n):
-            other = (i > j) if uplo == "U" else (i < j)
-            if other:
-                out[(i + j * lda) if layout == "C" else (i * lda + j)] = np.nan
+    i, j = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
+    other = (i > j) if uplo == "U" else (i < j)
+    idx = (i + j * lda) if layout == "C" else (i * lda + j)
+    out[idx[other]] = np.nan
     return out
 
 
 def full_sketch(cuda, side, layout, d, n, M, dtype=np.float64, major="L", key=5, alpha=0.75, beta=0.0, B0=None,
-                S_buff=None):
+                S_buff=None, opA="N"):
+    """The full-storage product. opA="T" is the same product for a bitwise-symmetric M (A^T = A) and
+    makes A the operand that is contiguous along the contracted index for (side L, RowMajor) and
+    (side R, ColMajor), so the same kernel as the one-triangle path computes it (with split-K at
+    K >= 2048 the splits then agree too)."""
     lda = n
     A = dev(store(M, layout, lda).astype(dtype), cuda)
     sr, sc = (d, n) if side == "L" else (n, d)
@@ -152,9 +151,9 @@ def full_sketch(cuda, side, layout, d, n, M, dtype=np.float64, major="L", key=5,
     ldb = br if layout == "C" else bc
     B = dev(B0.copy() if B0 is not None else np.zeros(br * bc, dtype), cuda)
     if side == "L":
-        rb.sketch_general_left(layout, "N", "N", d, n, n, dtype(alpha), S, A, lda, dtype(beta), B, ldb, ro_s=2, co_s=4)
+        rb.sketch_general_left(layout, "N", opA, d, n, n, dtype(alpha), S, A, lda, dtype(beta), B, ldb, ro_s=2, co_s=4)
     else:
-        rb.sketch_general_right(layout, "N", "N", n, d, n, dtype(alpha), A, lda, S, dtype(beta), B, ldb, ro_s=2,
+        rb.sketch_general_right(layout, opA, "N", n, d, n, dtype(alpha), A, lda, S, dtype(beta), B, ldb, ro_s=2,
                                 co_s=4)
     return host(B), S, ldb
 
@@ -196,13 +195,17 @@ def test_sketch_symmetric_triangle_vs_oracle(cuda):
 @pytest.mark.parametrize("layout", ["C", "R"])
 @pytest.mark.parametrize("uplo", ["U", "L"])
 @pytest.mark.parametrize("fmt", ["F", "P"])
-def test_sksy_tri_full_and_packed(cuda, side, layout, uplo, fmt):
-    """rbh_sksy_tri: only triangle uplo is read (the other holds NaN), beta != 0, full or packed."""
-    d, n = 80, 600
+@pytest.mark.parametrize("n", [600, 2560])
+def test_sksy_tri_full_and_packed(cuda, side, layout, uplo, fmt, n):
+    """rbh_sksy_tri: only triangle uplo is read (the other holds NaN), beta != 0, full or packed.
+    n = 2560 spans five 512-row memory tiles (every tile class of the one-triangle kernel: inside
+    the triangle, mirrored and straddling the diagonal, several times per output tile)."""
+    d = 80
     M = sym_full(n, 6)
     br, bc = (d, n) if side == "L" else (n, d)
     B0 = np.random.default_rng(2).standard_normal(br * bc)
-    ref, S, ldb = full_sketch(cuda, side, layout, d, n, M, beta=-0.5, B0=B0)
+    opA = "T" if (side == "L") == (layout == "R") else "N"
+    ref, S, ldb = full_sketch(cuda, side, layout, d, n, M, beta=-0.5, B0=B0, opA=opA)
     if fmt == "F":
         lda = n + 3
         A = poison_other_triangle(store(M, layout, lda), n, lda, layout, uplo)

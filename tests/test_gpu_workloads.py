@@ -147,6 +147,33 @@ def test_c5_sksy_with_symmetry_check(cuda):
     del A
 
 
+def test_c5_packed_as_worded(cuda):
+    """configs[4] as worded: sksy f64, d=512 on PACKED-symmetric A, n=16384 (the one-triangle kernel
+    on BLAS packed upper storage, rbh_sksy_tri). Three column slices vs the oracle's lskge3 on the
+    full matrix within E, the row sums, and bitwise equality with sketch_symmetric on full storage
+    (sksy.hh:520-537; test/test_matmul_wrappers/test_sketch_symmetric.cc:86-161 checks against symm)."""
+    d, n = 512, 16384
+    A = device_A(cuda, n, n, torch.float64)
+    Am = A.view(n, n)
+    A.copy_(((Am + Am.t()) * 0.5).reshape(-1))
+    # ColMajor upper packed: column j's A(0..j, j) in turn (row j of the view is column j of A)
+    AP = Am.masked_select(torch.ones(n, n, dtype=torch.bool, device=cuda).tril()).contiguous()
+    assert AP.numel() == n * (n + 1) // 2
+    S = rb.DenseSkOp(rb.DenseDist(d, n), rb.RNGState(0))
+    B = torch.empty(d * n, dtype=torch.float64, device=cuda)
+    rb.sketch_symmetric_tri("C", "L", "U", "P", d, n, 1.0, S, AP, 0, 0.0, B, d)
+    for j0 in (0, 7000, n - 96):
+        cols = host(Am[j0:j0 + 96]).reshape(-1)
+        check_dense_slice(B, cols, d, n, n, j0, 96, np.float64)
+    check_row_sums(B, A, d, n, n, d, 0, np.float64)
+    del AP
+    Bf = torch.empty(d * n, dtype=torch.float64, device=cuda)
+    rb.sketch_symmetric_left("C", d, n, 1.0, S, A, n, 0.0, Bf, d)
+    got, ref = host(B), host(Bf)
+    assert np.array_equal(got.view(np.uint64), ref.view(np.uint64)), f"{np.sum(got != ref)} differ"
+    del A
+
+
 def test_c3_saso_slices_bitwise(cuda):
     """configs[2]: SASO vec_nnz=8 f64, d=1024, A 16384^2: the whole sketch in one call, column slices
     bitwise against the oracle's left_spmm (ascending-column scatter, csc_spmm_impl.hh:43-65)."""
