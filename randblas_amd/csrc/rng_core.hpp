@@ -135,6 +135,13 @@ RB_HD float uneg11f(uint32_t u) {
 // ------------------------------------------------------------------------------------------
 RB_HD uint32_t f32_bits(float f) { union { float f; uint32_t u; } c; c.f = f; return c.u; }
 RB_HD float f32_from(uint32_t u) { union { float f; uint32_t u; } c; c.u = u; return c.f; }
+// x with its sign bit xor-ed by `sign` (0 or 0x80000000): x * -1.0 exactly when sign is set
+RB_HD double f64_xor_sign(double x, uint32_t sign) {
+    union { double d; uint64_t u; } c;
+    c.d = x;
+    c.u ^= (uint64_t)sign << 32;
+    return c.d;
+}
 
 #if defined(__HIPCC__)
 #define RB_FMA(a, b, c) __builtin_fma((a), (b), (c))
@@ -170,8 +177,10 @@ RB_HD void rb_sincosf(float y, float &sin_out, float &cos_out) {
     const double r = xd * SC_HPI_INV;
     const int n = ((int32_t)r + 0x800000) >> 24;
     const double x = RB_FMA(-(double)n, SC_HPI, xd);
-    const double sgn = ((n + 1) & 2) ? -1.0 : 1.0;       // sign[n&3] = {1,-1,-1,1}
-    const double xs = x * sgn;
+    // xs = x * sign[n & 3], sign = {1, -1, -1, 1}; the signs below are applied as bit operations
+    // (the same values: multiplying by -1 only flips the sign bit), which keeps the draw free of
+    // compare-and-select pairs
+    const double xs = f64_xor_sign(x, ((uint32_t)(n + 1) & 2u) << 30);
     const double x2 = x * x;
     // sincosf_poly(xs, x2, ...)
     const double x4 = x2 * x2;
@@ -185,9 +194,11 @@ RB_HD void rb_sincosf(float y, float &sin_out, float &cos_out) {
     const double c = RB_FMA(x4, SC_C2, cc1);
     const float ps = (float)RB_FMA(x5, ss1, s);
     const float pc0 = (float)RB_FMA(x6, cc2, c);
-    const float pc = (n & 2) ? -pc0 : pc0;
-    sin_out = (n & 1) ? pc : ps;
-    cos_out = (n & 1) ? ps : pc;
+    const uint32_t pcb = f32_bits(pc0) ^ (((uint32_t)n & 2u) << 30);   // (n & 2) ? -pc0 : pc0
+    const uint32_t psb = f32_bits(ps);
+    const uint32_t odd = 0u - ((uint32_t)n & 1u);                       // all ones for odd n
+    sin_out = f32_from((pcb & odd) | (psb & ~odd));
+    cos_out = f32_from((psb & odd) | (pcb & ~odd));
 }
 
 // logf for normal positive finite x (the Box-Muller radius argument is u01 in [2^-33, 1]; all 2^32
@@ -249,6 +260,24 @@ RB_HD float rb_sqrtf(float v) {
 #endif
 }
 
+// The Box-Muller radius sqrt(-2 log u) for u = u01(w): its argument is -0 (u = 1) or in
+// [2^-23, 46]. On the device: v_sqrt_f32 (within 1 ulp) and the residual fix-up of the compiler's
+// correctly rounded sqrtf, without that sequence's scaling for tiny inputs and its special-value
+// cases, none of which the argument reaches (-0 passes through the fix-up unchanged: its lower
+// neighbour is a NaN, its upper one gives a zero residual). tools/micro/check_sqrt.hip checks it
+// against the correctly rounded sqrt for every float in [0, 64] and -0.
+RB_HD float rb_sqrtf_bm(float v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float s = __builtin_amdgcn_sqrtf(v);
+    const float sd = f32_from(f32_bits(s) - 1u), su = f32_from(f32_bits(s) + 1u);
+    const float rd = __builtin_fmaf(-sd, s, v), ru = __builtin_fmaf(-su, s, v);
+    const float t = rd <= 0.0f ? sd : s;
+    return ru > 0.0f ? su : t;
+#else
+    return (float)sqrt((double)v);
+#endif
+}
+
 // r123::boxmuller(u0, u1) -> {r*sin(pi*x), r*cos(pi*x)}, x = uneg11(u0), r = sqrt(-2 log u01(u1)).
 RB_HD void boxmuller(uint32_t u0, uint32_t u1, float &g0, float &g1, const LogfEntry *tab = LOGF_TAB) {
 #if defined(__clang__)
@@ -257,7 +286,7 @@ RB_HD void boxmuller(uint32_t u0, uint32_t u1, float &g0, float &g1, const LogfE
     const float PIf = 3.1415926535897932f;
     float s, c;
     rb_sincosf(PIf * uneg11f(u0), s, c);
-    const float r = rb_sqrtf(-2.0f * rb_logf_tab(u01f(u1), tab));
+    const float r = rb_sqrtf_bm(-2.0f * rb_logf_tab(u01f(u1), tab));
     g0 = s * r;
     g1 = c * r;
 }

@@ -545,6 +545,9 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 // element (o, k) outside it is the stored (k, o). A K step's 512 x 16 tile is then wholly inside
 // the triangle (loaded as usual), wholly outside (loaded from the mirror tile, which is contiguous
 // along o, and transposed into the LDS image), or straddles the diagonal (per-element select).
+#ifndef RBH_WIDE_DMA
+#define RBH_WIDE_DMA 0
+#endif
 template <int GK, int FAMILY, bool GX, int TRI, bool SPLIT, bool GMAT>
 __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
     typedef double T;
@@ -589,19 +592,49 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
     typedef typename Vec2<T>::type v2_t;
     v2_t rs[4];
     const char *mtile = (const char *)(mptr + mo0 * mop.so);
-    // byte offset of vector e = voff0 + e * vstep, clamped to the last row of the operand
+    // The memory tile is read through a buffer resource based at its first row: the per-lane byte
+    // offsets are fixed for the whole loop (precomputed, rows past the operand clamped to its last
+    // row) and the k offset of a step rides in the SGPR soffset, so a step's staging loads cost no
+    // address arithmetic. (On gfx950 every instruction a wave issues beside the f64 MFMAs adds to
+    // the step: tools/micro/mfma_coexec.hip.)
+    const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc((void *)mtile, (short)0, -1, 0x00020000);
     const uint32_t vstep = (uint32_t)(64 * mop.so * (int64_t)sizeof(T));
     const uint32_t voff0 = (uint32_t)(((tid >> 3) * mop.so + 2 * (tid & 7)) * (int64_t)sizeof(T));
     const uint32_t vmax = (uint32_t)(((mnO - 1 - mo0) * mop.so + 2 * (tid & 7)) * (int64_t)sizeof(T));
     const int lwoff = (tid >> 3) * BK + 2 * ((tid & 7) ^ ((tid >> 4) & 7));   // doubles, + 1024 * e
+#if RBH_WIDE_DMA
+    // LDS-DMA staging: wave w's copy e fills rows 8 (w + 8 e) .. + 7 of the image (1 KB); lane l
+    // takes row 8 (w + 8 e) + (l >> 3), slot l & 7, i.e. 16-B vector (l & 7) ^ swz(row)
+    uint32_t doff[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int o = 8 * (wave + 8 * e) + (lane >> 3);
+        const int v = (lane & 7) ^ ((o >> 1) & 7);
+        const int64_t orow = mo0 + o < mnO ? o : mnO - 1 - mo0;
+        doff[e] = (uint32_t)((orow * mop.so + 2 * v) * (int64_t)sizeof(T));
+    }
+    auto rdma = [&](int64_t k0, int st) {
+        const int64_t ck0 = k0 < p.K ? k0 : p.K - BK;
+        const uint32_t soff = (uint32_t)(ck0 * (int64_t)sizeof(T));
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                mrsrc, (__attribute__((address_space(3))) void *)(lds + st * MS + 8 * (wave + 8 * e) * BK), 16, doff[e],
+                soff, 0, 0);
+    };
+#endif
+    uint32_t voff[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const uint32_t vo = voff0 + (uint32_t)e * vstep;
+        voff[e] = vo < vmax ? vo : vmax;
+    }
     auto rload = [&](int64_t k0, int half) {
         const int64_t ck0 = k0 < p.K ? k0 : p.K - BK;
-        const char *base = mtile + ck0 * (int64_t)sizeof(T);
+        const uint32_t soff = (uint32_t)(ck0 * (int64_t)sizeof(T));
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const uint32_t vo = voff0 + (uint32_t)(4 * half + e) * vstep;
-            rs[e] = *reinterpret_cast<const v2_t *>(base + (vo < vmax ? vo : vmax));
-        }
+        for (int e = 0; e < 4; ++e)
+            rs[e] = __builtin_bit_cast(v2_t, __builtin_amdgcn_raw_buffer_load_b128(mrsrc, voff[4 * half + e], soff, 0));
     };
     auto rstore = [&](int st, int half) {
         T *dst = lds + st * MS + lwoff;
@@ -684,25 +717,22 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
             *reinterpret_cast<v2_t *>(dst + BK) = r1;
         }
     };
-    // draw of the 64 x 16 generated tile for step kt (waves 0-3, one Philox call per lane). (A
-    // counter precomputed per lane, advanced by a uniform step, saves a few VALU but costs the
-    // 4 VGPRs this kernel does not have.)
+    // draw of the 64 x 16 generated tile for step kt (waves 0-3, one Philox call per lane): the
+    // lane's counter at step 0 is precomputed (cbase), a step adds the uniform kt * inc
     T gv[4];
     const bool glane_ok = GK == GEN_OK ? go0 + (tid >> 2) < gnO : true;
     const bool gtile_full = go0 + BG <= gnO;
+    uint32_t cbase[4];
+    {
+        uint64_t off;
+        if (GK == GEN_OK) off = (uint64_t)(gop.pr0 + go0 + (tid >> 2)) * gop.stride + (uint64_t)(gop.pc0 >> 2) + (tid & 3);
+        else off = (uint64_t)(gop.pr0 + ((tid >> 4) & 15)) * gop.stride + (uint64_t)((gop.pc0 + go0) >> 2) + (tid & 15);
+        rb::ctr_add(gop.ctr, off, cbase);
+    }
+    const uint64_t cinc = GK == GEN_OK ? (uint64_t)(BK / 4) : (uint64_t)BK * gop.stride;
     auto draw = [&](int64_t kt) {
         uint32_t c[4];
-        {
-            uint64_t off;
-            if (GK == GEN_OK) {
-                const int o = tid >> 2, q = tid & 3;
-                off = (uint64_t)(gop.pr0 + go0 + o) * gop.stride + (uint64_t)(gop.pc0 >> 2) + q + (uint64_t)kt * (BK / 4);
-            } else {
-                const int k = tid >> 4, q = tid & 15;
-                off = (uint64_t)(gop.pr0 + kt * BK + k) * gop.stride + (uint64_t)((gop.pc0 + go0) >> 2) + q;
-            }
-            rb::ctr_add(gop.ctr, off, c);
-        }
+        rb::ctr_add(cbase, (uint64_t)kt * cinc, c);
         const rb::u32x4 w = rb::philox4x32_uk<10>(c[0], c[1], c[2], c[3], gop.key[0], gop.key[1]);
         float sm[4];
         rb::sample4<FAMILY>(w, sm, tab);
@@ -773,7 +803,11 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
         const int c0 = tclass(kt0 * BK);
         rload_tri(kt0 * BK, 0, c0); rstore_tri(0, 0, c0); rload_tri(kt0 * BK, 1, c0); rstore_tri(0, 1, c0);
     } else {
+#if RBH_WIDE_DMA
+        rdma(kt0 * BK, 0);
+#else
         rload(kt0 * BK, 0); rstore(0, 0); rload(kt0 * BK, 1); rstore(0, 1);
+#endif
     }
     if (GMAT) { gload(kt0); gstore_m(0); }
     else if (wave < 4) { draw(kt0); gstore(0); }
@@ -792,14 +826,20 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
         const int64_t kn = (kt + 1) * BK;
         const int cn = tclass(kn);
         if (TRI) rload_tri(kn, 0, cn);
+#if RBH_WIDE_DMA
+        else rdma(kn, cur ^ 1);
+#else
         else rload(kn, 0);
+#endif
         if (GMAT) gload(kt + 1);
         else if (!GMAT && wave < 4) draw(kt + 1);
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             if (s == 2) {
                 if (TRI) { rstore_tri(cur ^ 1, 0, cn); rload_tri(kn, 1, cn); }
+#if !RBH_WIDE_DMA
                 else { rstore(cur ^ 1, 0); rload(kn, 1); }
+#endif
             }
             T gf[FA];
 #pragma unroll
@@ -817,7 +857,9 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
         if (GMAT) gstore_m(cur ^ 1);
         else if (wave < 4) gstore(cur ^ 1);
         if (TRI) rstore_tri(cur ^ 1, 1, cn);
+#if !RBH_WIDE_DMA
         else rstore(cur ^ 1, 1);
+#endif
         __syncthreads();
     }
     };
@@ -928,19 +970,17 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
     T gv[4];
     const bool glane_ok = GK == GEN_OK ? go0 + (tid >> 3) < gnO : true;
     const bool gtile_full = go0 + BG <= gnO;
+    uint32_t cbase[4];   // the lane's counter at step 0; a step adds the uniform kt * cinc
+    {
+        uint64_t off;
+        if (GK == GEN_OK) off = (uint64_t)(gop.pr0 + go0 + (tid >> 3)) * gop.stride + (uint64_t)(gop.pc0 >> 2) + (tid & 7);
+        else off = (uint64_t)(gop.pr0 + (tid >> 4)) * gop.stride + (uint64_t)((gop.pc0 + go0) >> 2) + (tid & 15);
+        rb::ctr_add(gop.ctr, off, cbase);
+    }
+    const uint64_t cinc = GK == GEN_OK ? (uint64_t)(KB32 / 4) : (uint64_t)KB32 * gop.stride;
     auto draw = [&](int64_t kt) {
         uint32_t c[4];
-        {
-            uint64_t off;
-            if (GK == GEN_OK) {
-                const int o = tid >> 3, q = tid & 7;
-                off = (uint64_t)(gop.pr0 + go0 + o) * gop.stride + (uint64_t)(gop.pc0 >> 2) + q + (uint64_t)kt * (KB32 / 4);
-            } else {
-                const int k = tid >> 4, q = tid & 15;
-                off = (uint64_t)(gop.pr0 + kt * KB32 + k) * gop.stride + (uint64_t)((gop.pc0 + go0) >> 2) + q;
-            }
-            rb::ctr_add(gop.ctr, off, c);
-        }
+        rb::ctr_add(cbase, (uint64_t)kt * cinc, c);
         const rb::u32x4 w = rb::philox4x32_uk<10>(c[0], c[1], c[2], c[3], gop.key[0], gop.key[1]);
         float sm[4];
         rb::sample4<FAMILY>(w, sm, tab);
@@ -1312,7 +1352,7 @@ static hipError_t launch_wide(const GemmProblem &p, hipStream_t s) {
 template <typename T>
 static bool wide_offsets_ok(const GemmProblem &p) {
     const MemOperand &m = p.xkind == MEM ? p.xm : p.ym;
-    return (int64_t)512 * m.so * (int64_t)sizeof(T) < ((int64_t)1 << 32);
+    return ((int64_t)512 * m.so + p.K) * (int64_t)sizeof(T) < ((int64_t)1 << 32);
 }
 
 template <typename T>
