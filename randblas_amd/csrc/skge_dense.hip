@@ -548,6 +548,9 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 #ifndef RBH_WIDE_DMA
 #define RBH_WIDE_DMA 0
 #endif
+#ifndef RBH_WIDE_LATEBAR
+#define RBH_WIDE_LATEBAR 1
+#endif
 template <int GK, int FAMILY, bool GX, int TRI, bool SPLIT, bool GMAT>
 __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
     typedef double T;
@@ -833,6 +836,7 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
 #endif
         if (GMAT) gload(kt + 1);
         else if (!GMAT && wave < 4) draw(kt + 1);
+        T gf3[FA], mf3[FB];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             if (s == 2) {
@@ -848,6 +852,13 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
             T mf[FB];
 #pragma unroll
             for (int c = 0; c < FB; ++c) mf[c] = Mc[mrow + 16 * c * BK + moff];
+            if (RBH_WIDE_LATEBAR && s == 3) {
+#pragma unroll
+                for (int a = 0; a < FA; ++a) gf3[a] = gf[a];
+#pragma unroll
+                for (int c = 0; c < FB; ++c) mf3[c] = mf[c];
+                continue;
+            }
 #pragma unroll
             for (int a = 0; a < FA; ++a)
 #pragma unroll
@@ -861,6 +872,16 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
         else rstore(cur ^ 1, 1);
 #endif
         __syncthreads();
+        // (RBH_WIDE_LATEBAR) the last sub-step's MFMAs come after the barrier, from fragments read
+        // before it: the waves leave the barrier with matrix work in hand, which covers the LDS
+        // latency of the next step's first fragment reads
+        if (RBH_WIDE_LATEBAR) {
+#pragma unroll
+            for (int a = 0; a < FA; ++a)
+#pragma unroll
+                for (int c = 0; c < FB; ++c)
+                    acc[a][c] = GX ? Mfma<T>::mma(mf3[c], gf3[a], acc[a][c]) : Mfma<T>::mma(gf3[a], mf3[c], acc[a][c]);
+        }
     }
     };
     k_loop();
