@@ -65,6 +65,13 @@ int rbh_is_device_pointer(const void *p);
 void rbh_kernel_timing_enable(int on);
 int rbh_kernel_timing_collect(float *ms, int max);
 
+/* Workspaces (no reference counterpart): the library keeps the device blocks its calls carve
+ * workspaces from, one arena per (device, stream), so repeated calls pay no allocation. This
+ * synchronises `stream` and frees its arena's idle blocks; stream == NULL does so for every stream
+ * of the current device (call it after destroying streams the library has seen). The library also
+ * releases idle blocks by itself before its retained bytes on a device would pass 2 GiB. */
+int rbh_release_workspaces(void *stream);
+
 /* ---- RNG state bookkeeping --------------------------------------------------------------- */
 /* dense::compute_next_state (dense_skops.hh:172-191). */
 int rbh_dense_next_state(const rbh_dense_dist *D, const rbh_state *seed, rbh_state *next);

@@ -108,6 +108,7 @@ for _t, _ct in (("f64", ctypes.c_double), ("f32", ctypes.c_float)):
     getattr(lib, f"rbh_spmm_right_{_t}").argtypes = [c_char, c_char, c_char, c_i64, c_i64, c_i64, _ct, c_vp, c_i64] + \
         _spm + [_ct, c_vp, c_i64, c_vp]
 lib.rbh_is_device_pointer.argtypes = [c_vp]
+lib.rbh_release_workspaces.argtypes = [c_vp]
 for _t, _ct in (("f64", ctypes.c_double), ("f32", ctypes.c_float)):
     getattr(lib, f"rbh_sketch_symmetric_{_t}").argtypes = [c_char, c_char, c_i64, c_i64, _ct, P(DenseDistC),
                                                            P(RNGStateC), c_vp, c_char, c_i64, c_i64, c_vp, c_i64, _ct,
@@ -526,11 +527,19 @@ def abi_version() -> int:
     return int(lib.rbh_abi_version())
 
 
+def release_workspaces(stream=None) -> None:
+    """Synchronise and free the library's idle workspace blocks: those of `stream` (a torch stream
+    or a raw hipStream_t), or of every stream of the current device when None (rbh_release_workspaces)."""
+    if stream is not None and hasattr(stream, "cuda_stream"):
+        stream = stream.cuda_stream
+    _check(lib.rbh_release_workspaces(c_vp(stream) if stream else None))
+
+
 __all__ = [
     "RNGState", "DenseDist", "SparseDist", "DenseSkOp", "SparseSkOp", "RandBLASError", "fill_dense", "fill_sparse",
     "sketch_general", "sketch_general_left", "sketch_general_right", "sketch_symmetric_left",
     "sketch_symmetric_right", "require_symmetric", "dense_next_state", "sparse_next_state", "abi_version", "lib",
     "LIB_PATH", "kernel_timing", "kernel_times_ms", "sketch_vector", "sketch_vector_full", "COOMatrix",
     "CSRMatrix", "CSCMatrix", "sketch_sparse", "sketch_sparse_left", "sketch_sparse_right", "spmm",
-    "sketch_symmetric_tri",
+    "sketch_symmetric_tri", "release_workspaces",
 ]

@@ -81,6 +81,32 @@ struct Arena {
 std::map<std::pair<int, hipStream_t>, Arena> g_arenas;
 constexpr size_t WS_ALIGN = 256;
 constexpr size_t WS_MIN_BLOCK = (size_t)64 << 20;
+// Retained-bytes cap per device: before an arena grows past it, the device is synchronised and every
+// idle block of every arena of that device (streams the client may have destroyed included) is
+// released. rbh_release_workspaces releases on request.
+constexpr size_t WS_RETAIN_CAP = (size_t)2 << 30;
+
+// free the blocks of arena a that hold no live workspace (the caller has synchronised the work
+// that used them); the current block restarts empty
+void arena_release_idle(Arena &a) {
+    const char *cur = a.blocks.empty() ? nullptr : a.blocks.back().base;
+    for (size_t i = a.blocks.size(); i-- > 0;)
+        if (a.blocks[i].live == 0) {
+            (void)hipFree(a.blocks[i].base);
+            a.blocks.erase(a.blocks.begin() + (ptrdiff_t)i);
+            for (auto &w : a.live)
+                if (w.second > i) --w.second;
+        }
+    if (a.blocks.empty()) a.top = 0;
+    else if (a.blocks.back().base != cur) a.top = a.blocks.back().cap;   // a retired block: never bump into it
+}
+size_t retained_bytes(int dev) {
+    size_t t = 0;
+    for (auto &kv : g_arenas)
+        if (kv.first.first == dev)
+            for (auto &b : kv.second.blocks) t += b.cap;
+    return t;
+}
 }  // namespace
 hipError_t ws_alloc(void **p, size_t bytes, hipStream_t s) {
     *p = nullptr;
@@ -94,6 +120,11 @@ hipError_t ws_alloc(void **p, size_t bytes, hipStream_t s) {
         const size_t last = a.blocks.empty() ? 0 : a.blocks.back().cap;
         size_t cap = 2 * last > WS_MIN_BLOCK ? 2 * last : WS_MIN_BLOCK;
         if (cap < need) cap = need;
+        if (retained_bytes(dev) + cap > WS_RETAIN_CAP) {   // over the cap: release every idle block
+            (void)hipDeviceSynchronize();
+            for (auto &kv : g_arenas)
+                if (kv.first.first == dev && &kv.second != &a) arena_release_idle(kv.second);
+        }
         char *nb = nullptr;
         e = hipMalloc((void **)&nb, cap);
         if (e != hipSuccess) return e;
@@ -132,6 +163,24 @@ hipError_t ws_free(void *p, hipStream_t s) {
     a.blocks[bi].live--;
     // the current block empties: bump from its start again (stream order protects the reuse)
     if (bi + 1 == a.blocks.size() && a.blocks[bi].live == 0) a.top = 0;
+    return hipSuccess;
+}
+// rbh_release_workspaces: synchronise, then free the idle blocks of the stream's arena (all
+// arenas of the current device for a null stream)
+hipError_t ws_release(hipStream_t s, bool all) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    e = all ? hipDeviceSynchronize() : hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    for (auto it = g_arenas.begin(); it != g_arenas.end();) {
+        if (it->first.first == dev && (all || it->first.second == s)) {
+            arena_release_idle(it->second);
+            if (it->second.blocks.empty() && it->second.live.empty()) { it = g_arenas.erase(it); continue; }
+        }
+        ++it;
+    }
     return hipSuccess;
 }
 }  // namespace rbh
@@ -1191,6 +1240,12 @@ int sketch_symmetric(char layout, char side, int64_t d, int64_t n, T alpha, cons
 extern "C" {
 
 int rbh_abi_version(void) { return 1; }
+
+int rbh_release_workspaces(void *stream) {
+    const hipError_t e = ws_release((hipStream_t)stream, stream == nullptr);
+    if (e != hipSuccess) return set_error(RBH_ERR_HIP, "HIP error %s in rbh_release_workspaces", hipGetErrorName(e));
+    return RBH_OK;
+}
 
 void rbh_kernel_timing_enable(int on) {
     g_timing.enabled = on != 0;

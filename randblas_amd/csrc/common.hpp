@@ -84,9 +84,10 @@ hipError_t launch_fill_dense_f32(const GenOperand &g, int64_t n_rows_, int64_t n
 void timing_begin(hipStream_t s);
 void timing_end(hipStream_t s);
 
-// Stream-ordered workspaces (capi.cpp). They come from a pool private to this library, one per
-// device, so the client's default memory pool and its release threshold are never touched.
+// Stream-ordered workspaces (capi.cpp): one arena of hipMalloc blocks per (device, stream), private
+// to this library; ws_release frees the idle blocks (rbh_release_workspaces).
 hipError_t ws_alloc(void **p, size_t bytes, hipStream_t s);
 hipError_t ws_free(void *p, hipStream_t s);
+hipError_t ws_release(hipStream_t s, bool all);
 
 }  // namespace rbh

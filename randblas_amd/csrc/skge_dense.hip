@@ -33,12 +33,7 @@ constexpr int BK = 16;
 // waves that load a materialised operator tile in the wide kernels (see skge_wide_kernel)
 // (measured, same box, both orders: f64 C2 8 waves 8.49-8.53 ms, 1 8.52-8.54, 2 8.57-8.59, 4 8.61-8.63;
 // f32 C4 4 waves 4.36 ms, 2 4.51-4.53, 1 and 8 4.65-4.67)
-#ifndef RBH_GMAT_W
-#define RBH_GMAT_W 8
-#endif
-#ifndef RBH_GMAT32_W
-#define RBH_GMAT32_W 4
-#endif
+constexpr int GMAT_WAVES = 8, GMAT32_WAVES = 4;
 
 template <typename T> struct Mfma;
 template <> struct Mfma<double> {
@@ -545,12 +540,7 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 // element (o, k) outside it is the stored (k, o). A K step's 512 x 16 tile is then wholly inside
 // the triangle (loaded as usual), wholly outside (loaded from the mirror tile, which is contiguous
 // along o, and transposed into the LDS image), or straddles the diagonal (per-element select).
-#ifndef RBH_WIDE_DMA
-#define RBH_WIDE_DMA 0
-#endif
-#ifndef RBH_WIDE_LATEBAR
-#define RBH_WIDE_LATEBAR 1
-#endif
+
 template <int GK, int FAMILY, bool GX, int TRI, bool SPLIT, bool GMAT>
 __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
     typedef double T;
@@ -605,27 +595,6 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
     const uint32_t voff0 = (uint32_t)(((tid >> 3) * mop.so + 2 * (tid & 7)) * (int64_t)sizeof(T));
     const uint32_t vmax = (uint32_t)(((mnO - 1 - mo0) * mop.so + 2 * (tid & 7)) * (int64_t)sizeof(T));
     const int lwoff = (tid >> 3) * BK + 2 * ((tid & 7) ^ ((tid >> 4) & 7));   // doubles, + 1024 * e
-#if RBH_WIDE_DMA
-    // LDS-DMA staging: wave w's copy e fills rows 8 (w + 8 e) .. + 7 of the image (1 KB); lane l
-    // takes row 8 (w + 8 e) + (l >> 3), slot l & 7, i.e. 16-B vector (l & 7) ^ swz(row)
-    uint32_t doff[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const int o = 8 * (wave + 8 * e) + (lane >> 3);
-        const int v = (lane & 7) ^ ((o >> 1) & 7);
-        const int64_t orow = mo0 + o < mnO ? o : mnO - 1 - mo0;
-        doff[e] = (uint32_t)((orow * mop.so + 2 * v) * (int64_t)sizeof(T));
-    }
-    auto rdma = [&](int64_t k0, int st) {
-        const int64_t ck0 = k0 < p.K ? k0 : p.K - BK;
-        const uint32_t soff = (uint32_t)(ck0 * (int64_t)sizeof(T));
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                mrsrc, (__attribute__((address_space(3))) void *)(lds + st * MS + 8 * (wave + 8 * e) * BK), 16, doff[e],
-                soff, 0, 0);
-    };
-#endif
     uint32_t voff[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -767,7 +736,7 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
     // GMAT: the 64 x 16 generated tile comes from the materialised operand (launch_gemm), rows
     // clamped to the operand (rows past it only feed discarded outputs), into the same LDS rows the
     // draw fills.
-    constexpr int GMAT_W = RBH_GMAT_W;
+    constexpr int GMAT_W = GMAT_WAVES;
     // The wave test stays in the code even when every wave loads (GMAT_W = 8, the compiler cannot
     // prove wave < 8) for TRI == 0: the split basic block schedules C2 at 8.49-8.53 ms against 8.81
     // without it, while the one-triangle kernels run faster without it (C5p 4.97 against 5.90 ms).
@@ -806,11 +775,7 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
         const int c0 = tclass(kt0 * BK);
         rload_tri(kt0 * BK, 0, c0); rstore_tri(0, 0, c0); rload_tri(kt0 * BK, 1, c0); rstore_tri(0, 1, c0);
     } else {
-#if RBH_WIDE_DMA
-        rdma(kt0 * BK, 0);
-#else
         rload(kt0 * BK, 0); rstore(0, 0); rload(kt0 * BK, 1); rstore(0, 1);
-#endif
     }
     if (GMAT) { gload(kt0); gstore_m(0); }
     else if (wave < 4) { draw(kt0); gstore(0); }
@@ -829,11 +794,7 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
         const int64_t kn = (kt + 1) * BK;
         const int cn = tclass(kn);
         if (TRI) rload_tri(kn, 0, cn);
-#if RBH_WIDE_DMA
-        else rdma(kn, cur ^ 1);
-#else
         else rload(kn, 0);
-#endif
         if (GMAT) gload(kt + 1);
         else if (!GMAT && wave < 4) draw(kt + 1);
         T gf3[FA], mf3[FB];
@@ -841,9 +802,7 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
         for (int s = 0; s < 4; ++s) {
             if (s == 2) {
                 if (TRI) { rstore_tri(cur ^ 1, 0, cn); rload_tri(kn, 1, cn); }
-#if !RBH_WIDE_DMA
                 else { rstore(cur ^ 1, 0); rload(kn, 1); }
-#endif
             }
             T gf[FA];
 #pragma unroll
@@ -852,7 +811,7 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
             T mf[FB];
 #pragma unroll
             for (int c = 0; c < FB; ++c) mf[c] = Mc[mrow + 16 * c * BK + moff];
-            if (RBH_WIDE_LATEBAR && s == 3) {
+            if (s == 3) {
 #pragma unroll
                 for (int a = 0; a < FA; ++a) gf3[a] = gf[a];
 #pragma unroll
@@ -868,14 +827,12 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
         if (GMAT) gstore_m(cur ^ 1);
         else if (wave < 4) gstore(cur ^ 1);
         if (TRI) rstore_tri(cur ^ 1, 1, cn);
-#if !RBH_WIDE_DMA
         else rstore(cur ^ 1, 1);
-#endif
         __syncthreads();
-        // (RBH_WIDE_LATEBAR) the last sub-step's MFMAs come after the barrier, from fragments read
+        // (true) the last sub-step's MFMAs come after the barrier, from fragments read
         // before it: the waves leave the barrier with matrix work in hand, which covers the LDS
         // latency of the next step's first fragment reads
-        if (RBH_WIDE_LATEBAR) {
+        if (true) {
 #pragma unroll
             for (int a = 0; a < FA; ++a)
 #pragma unroll
@@ -1020,7 +977,7 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
     };
     // GMAT: the 64 x 32 tile from the materialised operand (rows clamped), loaded by the first
     // GMAT_W waves, 8 / GMAT_W vectors per lane, into the swizzled rows the GEN_OK draw fills
-    constexpr int GMAT_W = RBH_GMAT32_W;
+    constexpr int GMAT_W = GMAT32_WAVES;
     constexpr int VPL = 8 / GMAT_W;
     v4f gmv[VPL];
     const int grw = (tid & (64 * GMAT_W - 1)) / GMAT_W, gvc = (tid % GMAT_W) * VPL;
@@ -1113,17 +1070,11 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
         if (GMAT) gstore_m(cur ^ 1);
         else gstore(cur ^ 1);
         rstore(cur ^ 1, 1);
-        __syncthreads();
+        __syncthreads();   // (MFMAs moved after it, as in skge_wide_kernel, measured slower here)
     }
     };
-#ifndef RBH_W32_POS_A
-#define RBH_W32_POS_A 2
-#endif
-#ifndef RBH_W32_POS_B
-#define RBH_W32_POS_B 0
-#endif
-    if (((wave >> 2) & 1) == 0) k_loop(std::integral_constant<int, RBH_W32_POS_A>{});
-    else k_loop(std::integral_constant<int, RBH_W32_POS_B>{});
+    if (((wave >> 2) & 1) == 0) k_loop(std::integral_constant<int, 2>{});
+    else k_loop(std::integral_constant<int, 0>{});
 
     T *C = SPLIT ? (T *)p.partial + z * p.M * p.N : (T *)p.C;
     const int64_t ldc = SPLIT ? p.M : p.ldc;
@@ -1243,10 +1194,8 @@ static hipError_t launch_fused(const GemmProblem &p, hipStream_t s) {
 }
 
 // The fused fast path applies when the generated window starts on a Philox quad and the memory
-// operand takes 16-B loads along k (see skge_fused_kernel); RBH_NO_FUSED=1 forces the generic kernel.
+// operand takes 16-B loads along k (see skge_fused_kernel).
 static bool fused_ok(const GemmProblem &p) {
-    static const bool off = [] { const char *e = getenv("RBH_NO_FUSED"); return e && e[0] == '1'; }();
-    if (off) return false;
     if ((p.xkind == MEM) == (p.ykind == MEM)) return false;
     const GenOperand &g = p.xkind == MEM ? p.yg : p.xg;
     const int mode = p.xkind == MEM ? p.xmode : p.ymode;
@@ -1378,8 +1327,7 @@ static bool wide_offsets_ok(const GemmProblem &p) {
 
 template <typename T>
 static bool wide_ok(const GemmProblem &p) {
-    static const bool off = [] { const char *e = getenv("RBH_NO_WIDE"); return e && e[0] == '1'; }();
-    return sizeof(T) == 8 && !off && fused_ok(p) && p.K % BK == 0 && wide_offsets_ok<T>(p);
+    return sizeof(T) == 8 && fused_ok(p) && p.K % BK == 0 && wide_offsets_ok<T>(p);
 }
 
 template <int GK, int FAMILY, bool GX>
@@ -1428,11 +1376,10 @@ static hipError_t launch_wide32(const GemmProblem &p, hipStream_t s) {
     return e;
 }
 
-// f32 on the 32-deep wide kernel: K % 32 == 0 (RBH_NO_WIDE32=1 keeps the 16-deep fused kernel)
+// f32 on the 32-deep wide kernel: K % 32 == 0
 template <typename T>
 static bool wide32_ok(const GemmProblem &p) {
-    static const bool off = [] { const char *e = getenv("RBH_NO_WIDE32"); return e && e[0] == '1'; }();
-    return sizeof(T) == 4 && !off && fused_ok(p) && p.K % KB32 == 0 && wide_offsets_ok<T>(p);
+    return sizeof(T) == 4 && fused_ok(p) && p.K % KB32 == 0 && wide_offsets_ok<T>(p);
 }
 
 // One-triangle symmetric memory operand: the wide f64 kernel when the generated operand runs its
@@ -1492,20 +1439,14 @@ static hipError_t launch_gemm(const GemmProblem &p, hipStream_t s) {
     }
     if (fused_ok(p)) {
         // tile (generated x memory outer indices) and waves; f32 variants selectable for tuning
-#ifndef RBH_F32_TG
-// f32 (C4): 64 generated x 512 memory rows, one wave along the generated dimension. Each operator
-// entry is drawn once per 512 memory columns instead of 256, for the same 64 accumulators per
-// lane. Measured at C4 (d = 256 per GPU, m = n = 32768): 128 x 256 / 2 x 4 waves 6.10 ms,
-// 64 x 512 / 1 x 8 waves 5.46 ms, 64 x 512 / 1 x 4 waves 7.93 ms, 128 x 512 / 2 x 8 waves 9.91 ms;
-// 1024-wide tiles exceed the 160 KB of LDS.
-#define RBH_F32_TG 64
-#define RBH_F32_TM 512
-#define RBH_F32_WG 1
-#define RBH_F32_WMW 8
-#endif
+// f32 (where the 32-deep wide kernel does not apply): 64 generated x 512 memory rows, one wave
+// along the generated dimension. Each operator entry is drawn once per 512 memory columns instead of
+// 256, for the same 64 accumulators per lane. Measured at C4 (d = 256 per GPU, m = n = 32768):
+// 128 x 256 / 2 x 4 waves 6.10 ms, 64 x 512 / 1 x 8 waves 5.46 ms, 64 x 512 / 1 x 4 waves 7.93 ms,
+// 128 x 512 / 2 x 8 waves 9.91 ms; 1024-wide tiles exceed the 160 KB of LDS.
         constexpr bool F32 = sizeof(T) == 4;
-        constexpr int TG = F32 ? RBH_F32_TG : 128, TMW = F32 ? RBH_F32_TM : 256;
-        constexpr int WG = F32 ? RBH_F32_WG : 2, WMW = F32 ? RBH_F32_WMW : 4;
+        constexpr int TG = F32 ? 64 : 128, TMW = F32 ? 512 : 256;
+        constexpr int WG = F32 ? 1 : 2, WMW = F32 ? 8 : 4;
 #define RBH_FUSED(XK, YK, BM, BN, WMS, WNS)                                                    \
     return unif ? launch_fused<T, XK, YK, rb::UNIFORM, BM, BN, WMS, WNS>(p, s)                  \
                 : launch_fused<T, XK, YK, rb::GAUSSIAN, BM, BN, WMS, WNS>(p, s)

@@ -309,3 +309,22 @@ def test_materialised_equals_drawn_bitwise(cuda, monkeypatch, dtype):
         out.append(host(B))
     ut = np.uint64 if dtype == np.float64 else np.uint32
     assert np.array_equal(out[0].view(ut), out[1].view(ut))
+
+
+def test_release_workspaces(cuda):
+    """rbh_release_workspaces: a split-K sketch (which takes a workspace) on a side stream, the
+    stream's arena released, every arena released, the same sketch again: bitwise the same."""
+    d, n, m = 128, 512, 4096   # 16 output tiles, K >= 2048: split-K partials in a workspace
+    A = dev(O.random_matrix(m, n, 99), cuda)
+    S = rb.DenseSkOp(rb.DenseDist(d, m), rb.RNGState(0))
+    out = []
+    for rel in ("stream", "all"):
+        st = torch.cuda.Stream(device=cuda)
+        B = torch.empty(d * n, dtype=torch.float64, device=cuda)
+        with torch.cuda.stream(st):
+            rb.sketch_general_left("C", "N", "N", d, n, m, 1.0, S, A, m, 0.0, B, d, stream=st.cuda_stream)
+        rb.release_workspaces(st if rel == "stream" else None)
+        out.append(host(B))
+        del st
+    rb.release_workspaces()
+    assert np.array_equal(out[0].view(np.uint64), out[1].view(np.uint64))

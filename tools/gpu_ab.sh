@@ -1,6 +1,7 @@
 #!/bin/bash
 # GPU tests, then each config's bench line in the default build and with one environment variant
-# (ALT, e.g. ALT="RBH_MATERIALISE=1"). Every step has its own time limit; the first failure stops.
+# variant (ALT="ENV=val;ENV2=val2", e.g. ALT="RBH_MATERIALISE=1"). Every step has its own time
+# limit; the first failure stops.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp
@@ -20,8 +21,12 @@ if [ -n "${TESTS+x}" ]; then
 fi
 for c in ${CONFIGS:-c2}; do
     run "def_$c.log" 300 python -u bench.py --config "$c" --no-cpu-baseline && summ "def_$c.log"
-    if [ -n "${ALT:-}" ]; then
-        run "alt_$c.log" 300 env $ALT python -u bench.py --config "$c" --no-cpu-baseline && summ "alt_$c.log"
-    fi
+    i=0
+    IFS=';' read -ra alts <<< "${ALT:-}"
+    for a in "${alts[@]}"; do
+        [ -z "$a" ] && continue
+        run "alt${i}_$c.log" 300 env $a python -u bench.py --config "$c" --no-cpu-baseline && summ "alt${i}_$c.log"
+        i=$((i+1))
+    done
 done
 echo "=== all done"
