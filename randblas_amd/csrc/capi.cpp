@@ -731,7 +731,6 @@ int sparse_common(SparseApply &p, const rbh_sparse_dist *D, const rbh_state *see
     RBH_HIP(st.map_out(B, sizeof(T), layout, B_rows, B_cols, ldb, beta != (T)0, &dB));
     p.Y = dA;
     p.C = dB;
-    if (const char *ab = getenv("RBH_SASO_ABLATE")) p.ablate = atoi(ab);   // diagnostics only
     if (!rows) {   // sample the operator on the device, inside the apply
         RBH_REQUIRE(seed != nullptr);
         RBH_HIP(run_sparse_sampled_t<T>(p, make_sparse_gen(D, seed), sparse_nnz(D), s));

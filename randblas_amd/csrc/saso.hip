@@ -218,25 +218,41 @@ __global__ void coo_keys_kernel(int64_t nnz, const int64_t *rows, const int64_t 
     }
 }
 
-// vrp[v] = first sorted position whose virtual row is >= v (invalid keys sort last); kl = k % SP_KC;
-// rec = the uniform-value apply's entry record (sections 4, 5): panel byte offset of k % SP_KC
-// (k * kmul), the accumulator register index of the row within its wave, sign of the value.
-template <typename T>
-__global__ void rowptr_kernel(int64_t nnz, const uint64_t *keys, const T *kv, int64_t NV, int64_t M, int32_t *vrp,
-                              uint16_t *kl, uint32_t *rec, uint32_t kmul) {
-    const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (e > nnz) return;
+// ptr[v] (0 <= v <= NV) = the first sorted position whose class key >> shift is >= v, invalid keys
+// (~0) being class NV: one thread per class, a binary search over the sorted keys (a thread per
+// entry filling the gap up to its class would serialise on a sparse operator over many classes)
+__global__ void class_ptr_kernel(int64_t nnz, const uint64_t *keys, int shift, int64_t NV, int32_t *ptr) {
+    const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (v > NV) return;
     const uint64_t inval = ~(uint64_t)0;
-    const int64_t cur = (e < nnz && keys[e] != inval) ? (int64_t)(keys[e] / SP_KC) : NV;
-    const int64_t prev = (e == 0) ? -1 : ((keys[e - 1] != inval) ? (int64_t)(keys[e - 1] / SP_KC) : NV);
-    for (int64_t v = prev + 1; v <= cur && v <= NV; ++v) vrp[v] = (int32_t)e;
-    if (e < nnz && keys[e] != inval) {
-        const uint16_t k = (uint16_t)(keys[e] % SP_KC);
-        kl[e] = k;
-        const uint32_t row = (uint32_t)((keys[e] / SP_KC) % (uint64_t)M) % 32u;   // row within its wave
-        rec[e] = (sizeof(T) == 8 ? 2u * row : row) | (((uint32_t)k * kmul) << 8) |
-                 (signbit(kv[e]) ? 0x80000000u : 0u);
+    int64_t lo = 0, hi = nnz;   // first e in [0, nnz] with class(keys[e]) >= v
+    while (lo < hi) {
+        const int64_t mid = lo + (hi - lo) / 2;
+        const uint64_t k = keys[mid];
+        const int64_t c = k == inval ? NV : (int64_t)(k >> shift);
+        if (c < v) lo = mid + 1;
+        else hi = mid;
     }
+    ptr[v] = (int32_t)lo;
+}
+
+static hipError_t launch_class_ptr(int64_t nnz, const uint64_t *keys, int shift, int64_t NV, int32_t *ptr, hipStream_t s) {
+    hipLaunchKernelGGL(class_ptr_kernel, dim3((unsigned)((NV + 1 + 255) / 256)), dim3(256), 0, s, nnz, keys, shift, NV, ptr);
+    return hipGetLastError();
+}
+
+// per sorted entry: kl = k % SP_KC; rec = the uniform-value apply's entry record (sections 4, 5):
+// panel byte offset of k % SP_KC (k * kmul), the accumulator register index of the row within its
+// wave, sign of the value
+template <typename T>
+__global__ void entry_rec_kernel(int64_t nnz, const uint64_t *keys, const T *kv, int64_t M, uint16_t *kl,
+                                 uint32_t *rec, uint32_t kmul) {
+    const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (e >= nnz || keys[e] == ~(uint64_t)0) return;
+    const uint16_t k = (uint16_t)(keys[e] % SP_KC);
+    kl[e] = k;
+    const uint32_t row = (uint32_t)((keys[e] / SP_KC) % (uint64_t)M) % 32u;   // row within its wave
+    rec[e] = (sizeof(T) == 8 ? 2u * row : row) | (((uint32_t)k * kmul) << 8) | (signbit(kv[e]) ? 0x80000000u : 0u);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -488,11 +504,11 @@ __global__ __launch_bounds__(SA_NT) __attribute__((amdgpu_waves_per_eu(SA_WPE_DE
         const int32_t ebase = f.ebase;
         const int ecount = f.ecount;
         __syncthreads();
-        if (c + 1 < nchunks && !(p.ablate & 2)) {
+        if (c + 1 < nchunks) {
             sa_load<T, VP>(f, p, vrp, kl, kv, c + 1, j0, rb0, nrows, tid, sa_range(bnext));
             if (c + 2 < nchunks) bnext = sa_bounds(p, vrp, c + 2, rb0, nrows, lane);
         }
-        if (!(p.ablate & 1)) sa_compute<T>(acc, pcol, rec, rp, 0, min(ecount, SA_EMAX), wrow, lane);
+        sa_compute<T>(acc, pcol, rec, rp, 0, min(ecount, SA_EMAX), wrow, lane);
         // rare: more entries in this chunk than LDS holds -> further windows, in order
         for (int w = SA_EMAX; w < ecount; w += SA_EMAX) {
             __syncthreads();
@@ -991,7 +1007,7 @@ template <int N> __device__ __forceinline__ void wait_vm() {
 }
 
 #ifdef SD_PROF
-// Diagnostic build only (-DSD_PROF, tools/build_saso_var.sh + tools/saso_prof.py): per-phase cycle
+// Diagnostic build only (-DSD_PROF, tools/build_var.sh + tools/saso_prof.py): per-phase cycle
 // totals of the DMA apply, summed over waves: 1 record load + barrier, 2 copy issue, 3 bounds,
 // 4 later record windows, 5 walk; 6 entries, 7 wave-chunks.
 __device__ unsigned long long rbh_sd_prof[8];
@@ -1104,7 +1120,9 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
 #endif
         // a sampled operator has no duplicate (row, k): at most SU_R * KC entries per wave
         ne = ne < 0 ? 0 : (ne > SU_R * KC ? SU_R * KC : ne);
-        if (p.ablate & 1) ne = 0;   // ablate 1: no walk
+#ifdef SD_ABLATE_WALK
+        ne = 0;   // diagnostic build: no walk
+#endif
     };
     // Records come straight from HBM/L2 into SGPRs (scalar loads), SD_SW at a time. The loads and
     // their wait are one asm statement, so no SGPR destination is visible to the compiler before the
@@ -1194,7 +1212,9 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
         const int gofs_c = gofs, ne_c = ne;
         if (ch + 1 < nchunks) chunk_range(ch + 1, gofs, ne);   // bounds ch + 1: visible since this barrier
         if (ch + 2 < nchunks) dma_bounds(ch + 2);
-        if (ch + 1 < nchunks && !(p.ablate & 2)) dma_panel(ch + 1);   // ablate 2: no copies
+#ifndef SD_ABLATE_COPY   // diagnostic build: no copies
+        if (ch + 1 < nchunks) dma_panel(ch + 1);
+#endif
         SD_T(2);
         walk_chunk(ch, gofs_c, ne_c);
     }
@@ -1441,11 +1461,10 @@ extern "C" int rbh_diag_saso_prof(unsigned long long *out, int reset) {
 // The DMA kernel's conditions: f64, values +-1 (sampled operator: distinct entries), |alpha| = 1
 // (the panel is Y itself), Y contiguous along k or j in 16-B vectors.
 static bool dma_eligible(const SparseApply &p, bool &y_k) {
-    static const bool dma_off = [] { const char *e = getenv("RBH_NO_SASO_DMA"); return e && e[0] == '1'; }();
     constexpr int VEC = 2;
     y_k = p.ysk == 1 && (p.ysj % VEC) == 0 && (((uintptr_t)p.Y) % 16) == 0 && (p.K % VEC) == 0;
     const bool y_jd = p.ysj == 1 && (p.ysk % VEC) == 0 && (((uintptr_t)p.Y) % 16) == 0 && (p.N % VEC) == 0;
-    return p.unit_vals && (p.alpha == 1.0 || p.alpha == -1.0) && (y_k || y_jd) && !dma_off;
+    return p.unit_vals && (p.alpha == 1.0 || p.alpha == -1.0) && (y_k || y_jd);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1471,16 +1490,6 @@ __global__ void row_keys_kernel(int64_t nnz, const int64_t *rows, const int64_t 
     const uint64_t k = (uint64_t)(p.transposed ? wr : wc);
     keys[e] = in ? (i << 32) | k : ~(uint64_t)0;
     kv[e] = (T)p.alpha * vals[e];
-}
-
-// rp[i] = first sorted entry of row i (invalid keys sort last; rp[M] = the valid count)
-__global__ void row_ptr_kernel(int64_t nnz, const uint64_t *keys, int64_t M, int32_t *rp) {
-    const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (e > nnz) return;
-    const uint64_t inval = ~(uint64_t)0;
-    const int64_t cur = (e < nnz && keys[e] != inval) ? (int64_t)(keys[e] >> 32) : M;
-    const int64_t prev = (e == 0) ? -1 : ((keys[e - 1] != inval) ? (int64_t)(keys[e - 1] >> 32) : M);
-    for (int64_t r = prev + 1; r <= cur; ++r) rp[r] = (int32_t)e;
 }
 
 template <typename T>
@@ -1550,8 +1559,7 @@ static hipError_t run_sparse_gather(const SparseApply &p, const int64_t *rows, c
         err = rocprim::radix_sort_pairs(tmp, tmp_bytes, k_in, k_out, v_in, v_out, (size_t)nnz, 0, (unsigned)end_bit, s);
     }
     if (err == hipSuccess) {
-        hipLaunchKernelGGL(row_ptr_kernel, dim3((unsigned)((nnz + 1 + 255) / 256)), dim3(256), 0, s, nnz, k_out, p.M, rp);
-        err = hipGetLastError();
+        err = launch_class_ptr(nnz, k_out, 32, p.M, rp, s);   // rp[i]: row i's first entry, rp[M] the valid count
     }
     if (err == hipSuccess) {
         timing_begin(s);
@@ -1577,8 +1585,7 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
         }
     }
     {   // row gather (section 8) for very sparse operators over j-contiguous Y
-        static const bool gather_off = [] { const char *e = getenv("RBH_NO_SASO_GATHER"); return e && e[0] == '1'; }();
-        if (!gather_off && p.ysj == 1 && (double)nnz * GATHER_DENSITY < (double)p.M * (double)p.K &&
+        if (p.ysj == 1 && (double)nnz * GATHER_DENSITY < (double)p.M * (double)p.K &&
             p.K < ((int64_t)1 << 32) &&
             p.M < ((int64_t)1 << 31) && p.M * ((p.N + GA_NT * GA_CPT - 1) / (GA_NT * GA_CPT)) < ((int64_t)1 << 31))
             return run_sparse_gather<T>(p, rows, cols, vals, nnz, s);
@@ -1622,8 +1629,7 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
     constexpr int VEC = SuCfg<T>::VEC;
     const bool y_j = p.ysj == 1;
     const bool y_k = p.ysk == 1 && (p.ysj % VEC) == 0 && (((uintptr_t)p.Y) % 16) == 0 && (p.K % VEC) == 0;
-    static const bool unit_off = [] { const char *e = getenv("RBH_NO_SASO_UNIT"); return e && e[0] == '1'; }();
-    const bool unit = (y_j || y_k) && !unit_off;
+    const bool unit = y_j || y_k;
 
     err = hipMemsetAsync(ut, 0, sizeof(UniformTest<T>), s);
     if (err != hipSuccess) { (void)ws_free(ws, s); return err; }
@@ -1636,8 +1642,12 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
         err = rocprim::radix_sort_pairs(tmp, tmp_bytes, k_in, k_out, v_in, v_out, (size_t)nnz, 0, (unsigned)end_bit, s);
         if (err != hipSuccess) { (void)ws_free(ws, s); return err; }
     }
-    hipLaunchKernelGGL(rowptr_kernel<T>, dim3((unsigned)((nnz + 1 + 255) / 256)), dim3(256), 0, s, nnz, k_out, v_out,
-                       NV, p.M, vrp, kl, rec, (uint32_t)sizeof(T));
+    static_assert(SP_KC == 128, "class shift 7");
+    err = launch_class_ptr(nnz, k_out, 7, NV, vrp, s);
+    if (err != hipSuccess) { (void)ws_free(ws, s); return err; }
+    if (nnz > 0)
+        hipLaunchKernelGGL(entry_rec_kernel<T>, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, k_out, v_out,
+                           p.M, kl, rec, (uint32_t)sizeof(T));
     timing_begin(s);
     if (unit) {
         const int64_t nrb_u = (p.M + SU_ROWS - 1) / SU_ROWS;

@@ -25,7 +25,6 @@ struct SparseApply {
     int64_t ysk, ysj;
     void *C;
     int64_t crs, ccs;
-    int ablate;   // diagnostics only (env RBH_SASO_ABLATE): 1 = skip the entry walk, 2 = skip the panel loads
     int unit_vals;   // every value is +1 or -1 (operator sampled by fill_sparse in this call)
     int kcs;         // LDS-DMA apply (saso.hip section 5): log2 of its chunk depth; set by the apply itself
 };

@@ -584,13 +584,26 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
     // + 32-bit VGPR offset addressing), so the staging costs no VALU in the loop.
     typedef typename Vec2<T>::type v2_t;
     v2_t rs[4];
-    const char *mtile = (const char *)(mptr + mo0 * mop.so);
+    // ---- one-triangle memory operand (TRI != 0) ----
+    constexpr bool TKLE = TRI == 1 || TRI == 3, TPACK = TRI >= 3;
+    // stored row a of the triangle starts at element rowbase(a), column b of it sits at rowbase(a)
+    // + b: a so (full storage), a (a + 1) / 2 (packed, b <= a), a n - a (a + 1) / 2 (packed, b >= a;
+    // the row starts at column a). The launcher checks that every byte offset fits in 32 bits.
+    const uint32_t tso = (uint32_t)mop.so, tn = (uint32_t)p.tri_n;
+    auto rowbase = [&](uint32_t a) -> uint32_t {
+        if (TRI == 3) return a * (a + 1) / 2;
+        if (TRI == 4) return a * tn - a * (a + 1) / 2;
+        return a * tso;
+    };
+    const char *mtile = (const char *)(mptr + (TPACK ? 0 : mo0 * mop.so));
     // The memory tile is read through a buffer resource based at its first row: the per-lane byte
     // offsets are fixed for the whole loop (precomputed, rows past the operand clamped to its last
     // row) and the k offset of a step rides in the SGPR soffset, so a step's staging loads cost no
     // address arithmetic. (On gfx950 every instruction a wave issues beside the f64 MFMAs adds to
-    // the step: tools/micro/mfma_coexec.hip.)
+    // the step: tools/micro/mfma_coexec.hip.) A packed triangle is read the same way, through the
+    // per-lane offsets of its rows' starts.
     const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc((void *)mtile, (short)0, -1, 0x00020000);
+    const __amdgpu_buffer_rsrc_t mwhole = __builtin_amdgcn_make_buffer_rsrc((void *)mptr, (short)0, -1, 0x00020000);
     const uint32_t vstep = (uint32_t)(64 * mop.so * (int64_t)sizeof(T));
     const uint32_t voff0 = (uint32_t)(((tid >> 3) * mop.so + 2 * (tid & 7)) * (int64_t)sizeof(T));
     const uint32_t vmax = (uint32_t)(((mnO - 1 - mo0) * mop.so + 2 * (tid & 7)) * (int64_t)sizeof(T));
@@ -598,8 +611,13 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
     uint32_t voff[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-        const uint32_t vo = voff0 + (uint32_t)e * vstep;
-        voff[e] = vo < vmax ? vo : vmax;
+        if (TPACK) {
+            const int64_t o = mo0 + (tid >> 3) + 64 * e;
+            voff[e] = (rowbase((uint32_t)(o < mnO ? o : mnO - 1)) + 2 * (tid & 7)) * (uint32_t)sizeof(T);
+        } else {
+            const uint32_t vo = voff0 + (uint32_t)e * vstep;
+            voff[e] = vo < vmax ? vo : vmax;
+        }
     }
     auto rload = [&](int64_t k0, int half) {
         const int64_t ck0 = k0 < p.K ? k0 : p.K - BK;
@@ -613,17 +631,9 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) *reinterpret_cast<v2_t *>(dst + 1024 * (4 * half + e)) = rs[e];
     };
-    // ---- one-triangle memory operand (TRI != 0) ----
-    constexpr bool TKLE = TRI == 1 || TRI == 3, TPACK = TRI >= 3;
     const bool mfull = mo0 + BMM <= mnO;
-    // stored element (a, b) of the triangle (b <= a for TKLE, b >= a otherwise); 32-bit index
-    // arithmetic (the launcher checks that every index fits in 31 bits)
-    const uint32_t tso = (uint32_t)mop.so, tn = (uint32_t)p.tri_n;
-    auto sidx = [&](uint32_t a, uint32_t b) -> uint32_t {
-        if (TRI == 3) return b + a * (a + 1) / 2;
-        if (TRI == 4) return (b - a) + a * tn - a * (a - 1) / 2;
-        return a * tso + b;
-    };
+    // stored element (a, b) of the triangle (b <= a for TKLE, b >= a otherwise)
+    auto sidx = [&](uint32_t a, uint32_t b) -> uint32_t { return rowbase(a) + b; };
     auto eidx = [&](uint32_t o, uint32_t k) -> uint32_t {
         const bool in = TKLE ? k <= o : k >= o;
         return in ? sidx(o, k) : sidx(k, o);
@@ -635,37 +645,33 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
         if (TKLE) return k0 + BK - 1 <= mo0 ? 0 : (k0 >= mo0 + BMM ? 1 : 2);
         return k0 >= mo0 + BMM - 1 ? 0 : (k0 + BK - 1 < mo0 ? 1 : 2);
     };
+    // class 0 is the plain staging (packed rows through their per-lane row starts); class 1 loads
+    // a 2 x 2 block per load pair -- (o, o + 1) at k and at k + 1, stored at (k, o..o+1) and
+    // (k + 1, o..o+1), whose row starts are wave-uniform (SALU) -- transposed in registers by
+    // rstore_tri into the usual 16-B slots; class 2 selects per element
+    const uint32_t vmir = (uint32_t)((mo0 + 2 * (tid & 255)) * (int64_t)sizeof(T));
     auto rload_tri = [&](int64_t k0, int half, int cls) {
         const int64_t ck0 = k0 < p.K ? k0 : p.K - BK;
-        if (cls == 0 && !TPACK) { rload(k0, half); return; }
+        if (cls == 0) { rload(k0, half); return; }
         if (cls == 1) {
-            // mirror: a 2 x 2 block per load pair -- (o, o + 1) at k and at k + 1, stored at (k, o..o+1)
-            // and (k + 1, o..o+1) -- transposed in registers by rstore_tri into the usual 16-B slots
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
-                const uint32_t k = (uint32_t)ck0 + 2 * ((tid >> 8) + 2 * (2 * half + e)), o = (uint32_t)mo0 + 2 * (tid & 255);
-                const uint32_t i0 = sidx(k, o), i1 = sidx(k + 1, o);
-                if (!TPACK) {
-                    rs[2 * e] = *reinterpret_cast<const v2_t *>(mptr + i0);
-                    rs[2 * e + 1] = *reinterpret_cast<const v2_t *>(mptr + i1);
-                } else {
-                    rs[2 * e][0] = mptr[i0];
-                    rs[2 * e][1] = mptr[i0 + 1];
-                    rs[2 * e + 1][0] = mptr[i1];
-                    rs[2 * e + 1][1] = mptr[i1 + 1];
-                }
+                const uint32_t k = (uint32_t)ck0 + 2 * ((wave >> 2) + 2 * (2 * half + e));
+                const uint32_t s0 = rowbase(k) * (uint32_t)sizeof(T), s1 = rowbase(k + 1) * (uint32_t)sizeof(T);
+                rs[2 * e] = __builtin_bit_cast(v2_t, __builtin_amdgcn_raw_buffer_load_b128(mwhole, vmir, s0, 0));
+                rs[2 * e + 1] = __builtin_bit_cast(v2_t, __builtin_amdgcn_raw_buffer_load_b128(mwhole, vmir, s1, 0));
             }
             return;
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            uint32_t ia, ib;   // the vector's two elements, consecutive in storage for class 0
-            {                  // (o, k) and (o, k + 1) of the usual image
+            uint32_t ia, ib;   // (o, k) and (o, k + 1) of the usual image
+            {
                 int64_t o64 = mo0 + (tid >> 3) + 64 * (4 * half + e);
                 const uint32_t o = (uint32_t)(o64 < mnO ? o64 : mnO - 1);
                 const uint32_t k = (uint32_t)ck0 + 2 * (tid & 7);
-                if (cls == 0) { ia = sidx(o, k); ib = ia + 1; }
-                else { ia = eidx(o, k); ib = eidx(o, k + 1); }
+                ia = eidx(o, k);
+                ib = eidx(o, k + 1);
             }
             rs[e][0] = mptr[ia];
             rs[e][1] = mptr[ib];
@@ -1407,9 +1413,9 @@ static hipError_t launch_gemm_tri(const GemmProblem &p, hipStream_t s) {
     if (p.tri <= 2 && ((((uintptr_t)m.ptr) % 16) || (m.so & 1))) return hipErrorNotSupported;
     // tiles inside the triangle take the plain 32-bit byte-offset loads
     if (p.tri <= 2 && !wide_offsets_ok<double>(p)) return hipErrorNotSupported;
-    // 31-bit element indices in the kernel
+    // 32-bit byte offsets into the whole stored triangle in the kernel
     const int64_t n = p.tri_n, last = p.tri <= 2 ? (n - 1) * m.so + n : n * (n + 1) / 2;
-    if (last >= ((int64_t)1 << 31)) return hipErrorNotSupported;
+    if (last * (int64_t)sizeof(double) >= ((int64_t)1 << 32)) return hipErrorNotSupported;
     const bool unif = g.family == rb::UNIFORM;
     if (gx) return unif ? launch_wide_tri<rb::UNIFORM, true>(p, s) : launch_wide_tri<rb::GAUSSIAN, true>(p, s);
     return unif ? launch_wide_tri<rb::UNIFORM, false>(p, s) : launch_wide_tri<rb::GAUSSIAN, false>(p, s);
