@@ -72,6 +72,15 @@ int rbh_kernel_timing_collect(float *ms, int max);
  * releases idle blocks by itself before its retained bytes on a device would pass 2 GiB. */
 int rbh_release_workspaces(void *stream);
 
+/* Shard reassembly for multi-GPU sketching (no reference counterpart): an
+ * all-gather leaves nshards shards one after another, shard g being `rows` runs of `run` elements;
+ * this copies run i of row j of shard g, src[(g * rows + j) * run + i], to
+ * dst[g * shard_stride + j * row_stride + i] on `stream` (elem_bytes 4 or 8). Output-row shards
+ * of a ColMajor d x n sketch: run = d_loc, row_stride = d, shard_stride = d_loc; column shards:
+ * run = d, row_stride = d, shard_stride = n_loc * d. Device pointers. */
+int rbh_unpack_shards(const void *src, int64_t nshards, int64_t rows, int64_t run, void *dst, int64_t row_stride,
+                      int64_t shard_stride, int elem_bytes, void *stream);
+
 /* ---- RNG state bookkeeping --------------------------------------------------------------- */
 /* dense::compute_next_state (dense_skops.hh:172-191). */
 int rbh_dense_next_state(const rbh_dense_dist *D, const rbh_state *seed, rbh_state *next);

@@ -109,6 +109,7 @@ for _t, _ct in (("f64", ctypes.c_double), ("f32", ctypes.c_float)):
         _spm + [_ct, c_vp, c_i64, c_vp]
 lib.rbh_is_device_pointer.argtypes = [c_vp]
 lib.rbh_release_workspaces.argtypes = [c_vp]
+lib.rbh_unpack_shards.argtypes = [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, ctypes.c_int, c_vp]
 for _t, _ct in (("f64", ctypes.c_double), ("f32", ctypes.c_float)):
     getattr(lib, f"rbh_sketch_symmetric_{_t}").argtypes = [c_char, c_char, c_i64, c_i64, _ct, P(DenseDistC),
                                                            P(RNGStateC), c_vp, c_char, c_i64, c_i64, c_vp, c_i64, _ct,
@@ -535,11 +536,24 @@ def release_workspaces(stream=None) -> None:
     _check(lib.rbh_release_workspaces(c_vp(stream) if stream else None))
 
 
+def unpack_shards(src, nshards, rows, run, dst, row_stride, shard_stride, stream=None) -> None:
+    """Reassemble all-gathered shards on the device (rbh_unpack_shards): src holds nshards shards of
+    `rows` runs of `run` elements each; run i of row j of shard g goes to
+    dst[g * shard_stride + j * row_stride + i]. src and dst: 1-D device tensors of one dtype."""
+    if src.dtype != dst.dtype:
+        raise TypeError("unpack_shards: src and dst dtypes differ")
+    if nshards * rows * run > src.numel() or (nshards and rows and run and
+                                              (nshards - 1) * shard_stride + (rows - 1) * row_stride + run > dst.numel()):
+        raise ValueError("unpack_shards: shapes exceed the buffers")
+    _check(lib.rbh_unpack_shards(_ptr(src), nshards, rows, run, _ptr(dst), row_stride, shard_stride,
+                                 src.element_size(), _stream(dst, stream)))
+
+
 __all__ = [
     "RNGState", "DenseDist", "SparseDist", "DenseSkOp", "SparseSkOp", "RandBLASError", "fill_dense", "fill_sparse",
     "sketch_general", "sketch_general_left", "sketch_general_right", "sketch_symmetric_left",
     "sketch_symmetric_right", "require_symmetric", "dense_next_state", "sparse_next_state", "abi_version", "lib",
     "LIB_PATH", "kernel_timing", "kernel_times_ms", "sketch_vector", "sketch_vector_full", "COOMatrix",
     "CSRMatrix", "CSCMatrix", "sketch_sparse", "sketch_sparse_left", "sketch_sparse_right", "spmm",
-    "sketch_symmetric_tri", "release_workspaces",
+    "sketch_symmetric_tri", "release_workspaces", "unpack_shards",
 ]

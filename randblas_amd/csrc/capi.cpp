@@ -1246,6 +1246,18 @@ int rbh_release_workspaces(void *stream) {
     return RBH_OK;
 }
 
+int rbh_unpack_shards(const void *src, int64_t nshards, int64_t rows, int64_t run, void *dst, int64_t row_stride,
+                      int64_t shard_stride, int elem_bytes, void *stream) {
+    RBH_REQUIRE(elem_bytes == 4 || elem_bytes == 8);
+    RBH_REQUIRE(nshards >= 0 && rows >= 0 && run >= 0);
+    RBH_REQUIRE(row_stride >= run);
+    RBH_REQUIRE(shard_stride >= 0);
+    if (nshards == 0 || rows == 0 || run == 0) return RBH_OK;
+    RBH_REQUIRE(src != nullptr && dst != nullptr);
+    RBH_HIP(launch_unpack_shards(src, nshards, rows, run, dst, row_stride, shard_stride, elem_bytes, (hipStream_t)stream));
+    return RBH_OK;
+}
+
 void rbh_kernel_timing_enable(int on) {
     g_timing.enabled = on != 0;
     g_timing.used = 0;

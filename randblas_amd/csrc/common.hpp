@@ -90,4 +90,7 @@ hipError_t ws_alloc(void **p, size_t bytes, hipStream_t s);
 hipError_t ws_free(void *p, hipStream_t s);
 hipError_t ws_release(hipStream_t s, bool all);
 
+// shards.hip: dst[g * shard_stride + j * row_stride + i] = src[(g * rows + j) * run + i]
+hipError_t launch_unpack_shards(const void *src, int64_t nshards, int64_t rows, int64_t run, void *dst,
+                                int64_t row_stride, int64_t shard_stride, int elem_bytes, hipStream_t s);
 }  // namespace rbh

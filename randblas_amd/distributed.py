@@ -7,7 +7,13 @@ rtd/source/updates/index.rst:34). So rank g of G computes rows [g*d_loc, (g+1)*d
 B = S * A by calling sketch_general with ro_s = g*d_loc -- no operator data moves -- and the only
 exchange is the all-gather that reassembles B. That all-gather is pipelined with the compute:
 A's columns are cut into `chunks`; chunk c's shard is all-gathered (RCCL over xGMI on GPU, gloo
-on CPU in tests) while chunk c+1 is computed, then unpacked into the ColMajor d x n result.
+on CPU in tests) while chunk c+1 is computed, then unpacked into the ColMajor d x n result -- on
+the GPU by the library's HIP copy (rbh_unpack_shards, one pass over the gathered bytes), on CPU
+tensors (the gloo tests) by the equivalent strided torch copy.
+
+Every rank's operator rows are regenerated inside its fused GEMM (the default dense path keeps S
+out of HBM), so cutting A's columns into chunks adds no operator traffic: a chunk's output tiles
+draw the S tiles they need exactly as the unchunked call's tiles would.
 
 The per-shard compute is a callable so the same driver runs the HIP path (bench.py) and the CPU
 oracle (tests/test_distributed_cpu.py):  compute(ro_s, j0, j1, out)  writes the d_loc x (j1-j0)
@@ -19,6 +25,19 @@ from typing import Callable, List, Optional
 
 import torch
 import torch.distributed as dist
+
+
+def _unpack(src: torch.Tensor, nshards: int, rows: int, run: int, dst: torch.Tensor, row_stride: int,
+            shard_stride: int) -> None:
+    """dst[g*shard_stride + j*row_stride + i] = src[(g*rows + j)*run + i]: the HIP kernel for device
+    tensors, a strided torch copy for CPU tensors."""
+    if dst.is_cuda:
+        import randblas_amd as rb
+
+        rb.unpack_shards(src, nshards, rows, run, dst, row_stride, shard_stride)
+        return
+    view = dst.as_strided((nshards, rows, run), (shard_stride, row_stride, 1))
+    view.copy_(src[:nshards * rows * run].view(nshards, rows, run))
 
 
 class RowShardedSketch:
@@ -54,15 +73,13 @@ class RowShardedSketch:
                                                          async_op=True))
         if B_full is None:
             return
-        Bv = B_full.view(self.n, self.d_total)   # ColMajor d_total x n == row-major [n][d_total]
         for c, (j0, j1) in enumerate(self.cols):
             nc = j1 - j0
+            # ColMajor d_total x n: column j of rank g's shard lands at j * d_total + g * d_loc
             if self.world > 1:
                 works[c].wait()
-                src = self.gathered[c].view(self.world, nc, self.d_loc).permute(1, 0, 2).reshape(nc, self.d_total)
-            else:
-                src = self.local[c].view(nc, self.d_loc)
-            Bv[j0:j1].copy_(src)
+            src = self.gathered[c] if self.world > 1 else self.local[c]
+            _unpack(src, self.world, nc, self.d_loc, B_full[j0 * self.d_total:], self.d_total, self.d_loc)
 
 
 class ColumnShardedSketch:
@@ -106,11 +123,10 @@ class ColumnShardedSketch:
                                                          async_op=True))
         if B_full is None:
             return
-        Bv = B_full.view(self.world, self.n_loc, self.d)   # [rank][local column][row]
         for c, (j0, j1) in enumerate(self.cols):
             nc = j1 - j0
+            # [rank][local column][row]: rank g's column j0 + j at (g n_loc + j0 + j) d
             if self.world > 1:
                 works[c].wait()
-                Bv[:, j0:j1].copy_(self.gathered[c].view(self.world, nc, self.d))
-            else:
-                Bv[0, j0:j1].copy_(self.local[c].view(nc, self.d))
+            src = self.gathered[c] if self.world > 1 else self.local[c]
+            _unpack(src, self.world, nc, self.d, B_full[j0 * self.d:], self.d, self.n_loc * self.d)

@@ -28,3 +28,21 @@ def test_bench_relaunches_n_ranks():
 def test_bench_refuses_world_mismatch():
     r = _run(["--gpus", "4", "--dry-run"], env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2
+
+
+def test_bench_split_d_fixed_problem():
+    """--split-d keeps the problem (ns: d = 2048 rows in total) and gives each of 2 ranks half of it,
+    at row offsets 0 and 1024; the line says strong scaling."""
+    r = _run(["--gpus", "2", "--dry-run", "--config", "ns", "--split-d", "--steps", "1", "--warmup", "0"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")][0]
+    assert line["d"] == 2048 and line["d_per_gpu"] == 1024 and line["ro_s"] == [0, 1024]
+    assert line["scaling"] == "strong" and line["ranks_max"] == 1.0
+
+
+def test_bench_weak_scaling_default():
+    """Without --split-d every rank keeps the config's d (c2: 1024) and the job is world * d rows."""
+    r = _run(["--gpus", "2", "--dry-run", "--config", "c2", "--steps", "1", "--warmup", "0"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")][0]
+    assert line["d"] == 2048 and line["d_per_gpu"] == 1024 and line["scaling"] == "weak"
