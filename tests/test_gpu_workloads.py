@@ -82,6 +82,24 @@ def test_c1_full(cuda):
     check_dense_slice(B, host(A), d, m, n, 0, n, np.float64)
 
 
+def test_c1_rowmajor_within_bound(cuda):
+    """C1 runs split-K (16 output tiles, K = 4096): the slices are added in order by a deterministic
+    reduction, whose rounding differs from the unsplit kernel's. The same sketch asked for in
+    RowMajor (A and B stored transposed) must stay within the reference's bound E of the oracle and
+    so within 2E of the ColMajor result (RBH_SPLITK)."""
+    d, m, n = 128, 4096, 4096
+    A = device_A(cuda, m, n, torch.float64)
+    S = rb.DenseSkOp(rb.DenseDist(d, m), rb.RNGState(0))
+    B = torch.empty(d * n, dtype=torch.float64, device=cuda)
+    rb.sketch_general_left("C", "N", "N", d, n, m, 1.0, S, A, m, 0.0, B, d)
+    A_rm = A.view(n, m).t().contiguous().view(-1)        # the same logical A, RowMajor
+    B_rm = torch.empty(d * n, dtype=torch.float64, device=cuda)
+    rb.sketch_general_left("R", "N", "N", d, n, m, 1.0, S, A_rm, n, 0.0, B_rm, n)
+    B_rm_as_cm = B_rm.view(d, n).t().contiguous().view(-1)
+    check_dense_slice(B_rm_as_cm, host(A), d, m, n, 0, n, np.float64)
+    check_dense_slice(B, host(A), d, m, n, 0, n, np.float64)
+
+
 def test_c2_slices_and_row_sums(cuda):
     """configs[1]: d=1024, A 16384^2 f64 (the bench workload): three column slices + row sums."""
     d, m, n = 1024, 16384, 16384
