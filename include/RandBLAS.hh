@@ -17,8 +17,10 @@
 // (hipMalloc) are used in place. Link with -lrandblas_hip.
 //
 // A DenseSkOp whose buff is nullptr is regenerated from its Philox counters inside the fused MFMA
-// GEMM, tile by tile into LDS; it is not written to memory. fill_dense(S) and submatrix_as_blackbox
-// still fill a host buffer, as in the reference, after which the operator is applied from it.
+// GEMM, tile by tile into LDS; it is not written to memory (unless the opt-in environment switch
+// RBH_MATERIALISE=1 asks for the window to be drawn into a workspace first).
+// fill_dense(S) and submatrix_as_blackbox still fill a host buffer, as in the reference, after
+// which the operator is applied from it.
 #pragma once
 
 #include <algorithm>
