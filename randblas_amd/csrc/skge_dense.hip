@@ -638,12 +638,16 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
         const bool in = TKLE ? k <= o : k >= o;
         return in ? sidx(o, k) : sidx(k, o);
     };
-    // step class: 0 inside the triangle, 1 mirrored, 2 straddles the diagonal (or a partial tile)
+    // step class: 0 inside the triangle, 1 mirrored, 2 straddles the diagonal (or a partial tile).
+    // The class of step k0 is c_lo below k0 = kA, 2 in [kA, kB), c_hi from kB: two uniform 32-bit
+    // compares per step (every SALU instruction beside the f64 MFMAs costs issue time)
+    constexpr int C_LO = TKLE ? 0 : 1, C_HI = TKLE ? 1 : 0;
+    const int kA = __builtin_amdgcn_readfirstlane(!mfull ? -1 : (int)(TKLE ? mo0 - BK + 2 : mo0 - BK + 1));
+    const int kB = __builtin_amdgcn_readfirstlane(!mfull ? 0x7fffffff : (int)(TKLE ? mo0 + BMM : mo0 + BMM - 1));
     auto tclass = [&](int64_t k0) -> int {
         if (TRI == 0) return 0;
-        if (!mfull) return 2;
-        if (TKLE) return k0 + BK - 1 <= mo0 ? 0 : (k0 >= mo0 + BMM ? 1 : 2);
-        return k0 >= mo0 + BMM - 1 ? 0 : (k0 + BK - 1 < mo0 ? 1 : 2);
+        const int k = (int)k0;
+        return k < kA ? C_LO : (k < kB ? 2 : C_HI);
     };
     // class 0 is the plain staging (packed rows through their per-lane row starts); class 1 loads
     // a 2 x 2 block per load pair -- (o, o + 1) at k and at k + 1, stored at (k, o..o+1) and
@@ -654,15 +658,39 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
         const int64_t ck0 = k0 < p.K ? k0 : p.K - BK;
         if (cls == 0) { rload(k0, half); return; }
         if (cls == 1) {
+            // stored rows k (the pair's first) and k + 1: rowbase(k + 1) = rowbase(k) + step(k)
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
-                const uint32_t k = (uint32_t)ck0 + 2 * ((wave >> 2) + 2 * (2 * half + e));
-                const uint32_t s0 = rowbase(k) * (uint32_t)sizeof(T), s1 = rowbase(k + 1) * (uint32_t)sizeof(T);
+                const uint32_t k = __builtin_amdgcn_readfirstlane((uint32_t)ck0 + 2 * ((wave >> 2) + 2 * (2 * half + e)));
+                const uint32_t s0 = rowbase(k) * (uint32_t)sizeof(T);
+                const uint32_t s1 = s0 + (TRI == 3 ? k + 1 : (TRI == 4 ? tn - k - 1 : tso)) * (uint32_t)sizeof(T);
                 rs[2 * e] = __builtin_bit_cast(v2_t, __builtin_amdgcn_raw_buffer_load_b128(mwhole, vmir, s0, 0));
                 rs[2 * e + 1] = __builtin_bit_cast(v2_t, __builtin_amdgcn_raw_buffer_load_b128(mwhole, vmir, s1, 0));
             }
             return;
         }
+        if (mfull) {
+            // the diagonal block: element (o, k) is stored at rowbase(o) + k inside the triangle
+            // (the class-0 offset voff plus the uniform k offset) and at rowbase(k) + o outside;
+            // o - k is a per-lane constant plus the uniform mo0 - k0 plus 64 e
+            const uint32_t kl = (uint32_t)ck0 + 2 * (tid & 7);
+            const uint32_t rk0 = rowbase(kl) * (uint32_t)sizeof(T), rk1 = rowbase(kl + 1) * (uint32_t)sizeof(T);
+            const uint32_t sin = (uint32_t)((TPACK ? 0 : mo0 * mop.so) * (int64_t)sizeof(T) + ck0 * (int64_t)sizeof(T));
+            const uint32_t ob = (uint32_t)((mo0 + (tid >> 3)) * (int64_t)sizeof(T));
+            const int dk = (int)(mo0 - ck0) + (tid >> 3) - 2 * (tid & 7);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int E = 4 * half + e, dd = dk + 64 * E;   // o - k
+                const bool in0 = TKLE ? dd >= 0 : dd <= 0, in1 = TKLE ? dd >= 1 : dd <= 1;
+                const uint32_t om = ob + (uint32_t)(64 * E * sizeof(T));
+                const uint32_t ia = in0 ? voff[E] + sin : rk0 + om;
+                const uint32_t ib = in1 ? voff[E] + sin + (uint32_t)sizeof(T) : rk1 + om;
+                rs[e][0] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(mwhole, ia, 0, 0));
+                rs[e][1] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(mwhole, ib, 0, 0));
+            }
+            return;
+        }
+        // a partial tile: rows past the operand clamped, indices per element
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             uint32_t ia, ib;   // (o, k) and (o, k + 1) of the usual image
@@ -686,13 +714,14 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
         for (int e = 0; e < 2; ++e) {
             const int kp = (tid >> 8) + 2 * (2 * half + e), op = tid & 255;
             T *dst = lds + st * MS + 2 * op * BK + 2 * (kp ^ (op & 7));
-            v2_t r0, r1;
-            r0[0] = rs[2 * e][0];
-            r0[1] = rs[2 * e + 1][0];
-            r1[0] = rs[2 * e][1];
-            r1[1] = rs[2 * e + 1][1];
-            *reinterpret_cast<v2_t *>(dst) = r0;
-            *reinterpret_cast<v2_t *>(dst + BK) = r1;
+            // each loaded pair goes out as one ds_write2_b64 (its two halves to rows o and o + 1)
+            // straight from the load's registers; the empty asm keeps the compiler from merging
+            // adjacent slots of the two loads into a 16-B write, which needs register moves
+            dst[0] = rs[2 * e][0];
+            dst[BK] = rs[2 * e][1];
+            asm volatile("" ::: "memory");
+            dst[1] = rs[2 * e + 1][0];
+            dst[BK + 1] = rs[2 * e + 1][1];
         }
     };
     // draw of the 64 x 16 generated tile for step kt (waves 0-3, one Philox call per lane): the
@@ -792,13 +821,17 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
     const int mrow = (16 * FB * wmm + r) * BK;          // + 16 * c * BK per fragment c
     const int msw = (r >> 1) & 7;
     // (the loop as a lambda: measured 9.25 -> 8.93 ms at C2 against the same loop written inline)
-    auto k_loop = [&]() {
-    for (int64_t kt = kt0; kt < kt1; ++kt) {
+    // One-triangle operands run the loop in up to three phases, each with the class of the step it
+    // loads (kn) fixed at compile time: no per-step class test or switch (C5p: SALU per launch
+    // 1.36e8 against 0.41e8 of full storage before this)
+    auto k_loop = [&](auto cls_c, int64_t ka, int64_t kb) {
+    constexpr int CN = decltype(cls_c)::value;
+    for (int64_t kt = ka; kt < kb; ++kt) {
         const int cur = (int)((kt - kt0) & 1);
         const T *Mc = lds + cur * MS;
         const T *Gc = lds + 2 * MS + cur * GS;
         const int64_t kn = (kt + 1) * BK;
-        const int cn = tclass(kn);
+        constexpr int cn = CN;
         if (TRI) rload_tri(kn, 0, cn);
         else rload(kn, 0);
         if (GMAT) gload(kt + 1);
@@ -847,7 +880,19 @@ __global__ __launch_bounds__(512) void skge_wide_kernel(const GemmProblem p) {
         }
     }
     };
-    k_loop();
+    if (TRI) {
+        // steps kt whose next k0 = (kt + 1) BK lies below kA: C_LO; below kB: 2; the rest: C_HI
+        auto first_at = [&](int64_t kk) -> int64_t {   // first kt with (kt + 1) BK >= kk, clamped
+            const int64_t t = kk <= BK ? 0 : (kk + BK - 1) / BK - 1;
+            return t < kt0 ? kt0 : (t > kt1 ? kt1 : t);
+        };
+        const int64_t ktA = first_at(kA), ktB = kB == 0x7fffffff ? kt1 : first_at(kB);
+        k_loop(std::integral_constant<int, C_LO>(), kt0, ktA);
+        k_loop(std::integral_constant<int, 2>(), ktA, ktB);
+        k_loop(std::integral_constant<int, C_HI>(), ktB, kt1);
+    } else {
+        k_loop(std::integral_constant<int, 0>(), kt0, kt1);
+    }
 
     // split-K: alpha times this split's partial sum to partial[z] (M x N col-major); the reduction
     // adds the splits in order and applies beta
