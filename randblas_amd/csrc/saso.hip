@@ -905,15 +905,30 @@ __global__ __launch_bounds__(SU_NT) void saso_unit_kernel(const SparseApply p, c
 //    a flag ring instead of the barrier, a rotating or dedicated copy wave, copies interleaved
 //    with the walk, an L2 prefetch of the panel after next.
 // ------------------------------------------------------------------------------------------
-constexpr int SD_KC = 128;   // contracted indices per chunk
+#ifndef SD_KCS_DEF
+#define SD_KCS_DEF 7
+#endif
+#ifndef SD_NB_DEF
+#define SD_NB_DEF 2
+#endif
+#ifndef SD_PD_DEF
+#define SD_PD_DEF 1
+#endif
+constexpr int SD_KCS = SD_KCS_DEF;   // log2 of the chunk depth
+constexpr int SD_KC = 1 << SD_KCS;   // contracted indices per chunk
+constexpr int SD_NB = SD_NB_DEF;     // panel buffers (a ring)
+constexpr int SD_PD = SD_PD_DEF;     // panels in flight ahead of the walked one
+static_assert(SD_NB >= SD_PD + 1 && (SD_NB & (SD_NB - 1)) == 0, "ring: the walked panel plus the ones in flight");
+constexpr int SD_BR = 8;             // record-bound ring slots (chunks c + 1 .. c + SD_PD + 1 live)
+static_assert(SD_BR >= SD_PD + 2, "bounds ring");
 constexpr int SD_SW = 48;    // records per scalar-load window (C3: 0.708 ms with 32, 0.692 ms with 48)
 
 struct SdCfg {
     typedef double T;
     static constexpr int VEC = 16 / (int)sizeof(T);
     static constexpr int PANEL_B = SD_KC * SU_J * (int)sizeof(T);   // bytes per panel buffer
-    static constexpr int BND_OFF = 2 * PANEL_B;                     // record bounds: a ring of 4 chunks
-    static constexpr int MAIN_B = BND_OFF + 4 * 64 * 4;
+    static constexpr int BND_OFF = SD_NB * PANEL_B;                 // record bounds: a ring of SD_BR chunks
+    static constexpr int MAIN_B = BND_OFF + SD_BR * 64 * 4;
     static constexpr int EPI_B = SuCfg<T>::EPI * (int)sizeof(T);
     static constexpr int BYTES = MAIN_B > EPI_B ? MAIN_B : EPI_B;
     static constexpr uint32_t PAD = 64u;   // padding record: the dummy's register index, koff 0, sign +
@@ -991,6 +1006,18 @@ __device__ __forceinline__ void dma16(const void *g, uint32_t m0) {
                  : "s"(m0), "v"(g)
                  : "memory", "m0");
 }
+// The same copy through a buffer resource (16 B per lane from rsrc base + voff + soff): the per-lane
+// offsets stay fixed for the whole loop and a chunk's k offset rides in the SGPR soff, so a copy
+// costs no address arithmetic.
+typedef uint32_t sd_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void dma16_buf(sd_u32x4 rsrc, uint32_t voff, uint32_t soff, uint32_t m0) {
+    asm volatile("s_mov_b32 m0, %0\n\t"
+                 "s_nop 0\n\t"
+                 "buffer_load_dwordx4 %1, %2, %3 offen lds"
+                 :
+                 : "s"(m0), "v"(voff), "s"(rsrc), "s"(soff)
+                 : "memory", "m0");
+}
 __device__ __forceinline__ void dma4(const void *g, uint32_t m0) {
     asm volatile("s_mov_b32 m0, %0\n\t"
                  "s_nop 0\n\t"
@@ -1006,6 +1033,48 @@ template <int N> __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// Top of a chunk: the first record window (SD_SW = 48 records from rec into six SGPR octets),
+// this wave's copies down to N in flight, the barrier, then the window's wait (one statement:
+// no scalar load is in flight while the compiler counts its own LDS reads).
+typedef uint32_t sd_u32x8 __attribute__((ext_vector_type(8)));
+template <int N>
+__device__ __forceinline__ void sd_top(sd_u32x8 &r0, sd_u32x8 &r1, sd_u32x8 &r2, sd_u32x8 &r3, sd_u32x8 &r4,
+                                       sd_u32x8 &r5, const uint32_t *rec) {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+#if defined(SD_ABLATE_REC) || defined(SD_ABLATE_BAR)   // diagnostic builds (wrong results, timing only)
+#ifdef SD_ABLATE_REC
+#define SD_REC_ ""
+#else
+#define SD_REC_ "s_load_dwordx8 %0, %6, 0x0\n\ts_load_dwordx8 %1, %6, 0x20\n\ts_load_dwordx8 %2, %6, 0x40\n\t" \
+                "s_load_dwordx8 %3, %6, 0x60\n\ts_load_dwordx8 %4, %6, 0x80\n\ts_load_dwordx8 %5, %6, 0xa0\n\t"
+#endif
+#ifdef SD_ABLATE_BAR
+#define SD_BAR_ ""
+#else
+#define SD_BAR_ "s_barrier\n\t"
+#endif
+    asm volatile(SD_REC_ "s_waitcnt vmcnt(%7)\n\t" SD_BAR_ "s_waitcnt lgkmcnt(0)"
+                 : "+s"(r0), "+s"(r1), "+s"(r2), "+s"(r3), "+s"(r4), "+s"(r5)
+                 : "s"(rec), "n"(N)
+                 : "memory");
+#undef SD_REC_
+#undef SD_BAR_
+#else
+    asm volatile("s_load_dwordx8 %0, %6, 0x0\n\t"
+                 "s_load_dwordx8 %1, %6, 0x20\n\t"
+                 "s_load_dwordx8 %2, %6, 0x40\n\t"
+                 "s_load_dwordx8 %3, %6, 0x60\n\t"
+                 "s_load_dwordx8 %4, %6, 0x80\n\t"
+                 "s_load_dwordx8 %5, %6, 0xa0\n\t"
+                 "s_waitcnt vmcnt(%7)\n\t"
+                 "s_barrier\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&s"(r0), "=&s"(r1), "=&s"(r2), "=&s"(r3), "=&s"(r4), "=&s"(r5)
+                 : "s"(rec), "n"(N)
+                 : "memory");
+#endif
+}
+
 #ifdef SD_PROF
 // Diagnostic build only (-DSD_PROF, tools/build_var.sh + tools/saso_prof.py): per-phase cycle
 // totals of the DMA apply, summed over waves: 1 record load + barrier, 2 copy issue, 3 bounds,
@@ -1016,7 +1085,7 @@ __device__ unsigned long long rbh_sd_prof[8];
 #define SD_T(slot) do { } while (0)
 #endif
 
-template <bool YJ>
+template <bool YJ, bool BUF>
 __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, const int32_t *seg,
                                                          const uint32_t *rec32, int64_t nchunks, int64_t nrb,
                                                          int vec_out) {
@@ -1057,7 +1126,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
         for (int r = 0; r < SU_R; ++r) acc.set(r, (T)0);
     }
 
-    // record bounds of chunk cc: bnd[(cc & 3) * 64 + l] = start of wave l's records, l <= 16 (l = 16:
+    // record bounds of chunk cc: bnd[(cc % SD_BR) * 64 + l] = start of wave l's records, l <= 16 (l = 16:
     // end); seg[] has one entry per (chunk, group of SU_R rows), NG groups per chunk, and a closing
     // entry; wave 0 copies them (one instruction)
     const int64_t NG = (p.M + SU_R - 1) / SU_R;
@@ -1066,7 +1135,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
         if (wave == 0) {
             const int64_t l = lane < 16 ? lane : 16;
             const int64_t g = grp0 + l < NG ? grp0 + l : NG;
-            dma4(seg + cc * NG + g, lds0 + G::BND_OFF + (uint32_t)((cc & 3) * 256));
+            dma4(seg + cc * NG + g, lds0 + G::BND_OFF + (uint32_t)((cc & (SD_BR - 1)) * 256));
         }
     };
     // panel of chunk cc -> buffer cc & 1; 1 KB per instruction, NI per wave; out-of-range sources
@@ -1074,9 +1143,37 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     // are not stored)
     constexpr int NI = KC * SU_J * (int)sizeof(T) / 1024 / 16;
     static_assert(NI >= 1, "whole instructions per wave");
+    // BUF (Y along k, the launcher checked that 64 columns + K fit 32-bit byte offsets): the copies
+    // go through a buffer resource based at the column tile, per-lane offsets precomputed (columns
+    // past N clamped to the last one); a chunk that runs past K takes the clamped global form below
+    sd_u32x4 rsrc = {0u, 0u, 0u, 0u};
+    uint32_t bvoff[NI];
+    if (BUF) {
+        const int64_t jl = p.N - j0 < SU_J ? p.N - j0 : SU_J;
+        const uint64_t base = (uint64_t)(uintptr_t)(Y + j0 * p.ysj);
+        rsrc[0] = __builtin_amdgcn_readfirstlane((uint32_t)base);
+        rsrc[1] = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32) & 0xffffu);
+        rsrc[2] = __builtin_amdgcn_readfirstlane((uint32_t)(((jl - 1) * p.ysj + p.K) * (int64_t)sizeof(T)));
+        rsrc[3] = 0x00020000u;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            constexpr int COLB = KC * (int)sizeof(T), CPI = 1024 / COLB, SPC = COLB / 16;
+            const int inst = wave * NI + i;
+            const int col = inst * CPI + (int)lane / SPC;
+            const int v = ((int)lane % SPC) ^ (col & 15);
+            const int64_t cj = col < jl ? col : jl - 1;
+            bvoff[i] = (uint32_t)((cj * p.ysj + VEC * v) * (int64_t)sizeof(T));
+        }
+    }
     auto dma_panel = [&](int64_t cc) {
-        const uint32_t pb = lds0 + (uint32_t)((cc & 1) * G::PANEL_B);
+        const uint32_t pb = lds0 + (uint32_t)((cc & (SD_NB - 1)) * G::PANEL_B);
         const int64_t kc0 = cc * KC;
+        if (BUF && kc0 + KC <= p.K) {
+            const uint32_t soff = (uint32_t)(kc0 * (int64_t)sizeof(T));
+#pragma unroll
+            for (int i = 0; i < NI; ++i) dma16_buf(rsrc, bvoff[i], soff, pb + (uint32_t)((wave * NI + i) * 1024));
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             const int inst = wave * NI + i;
@@ -1110,7 +1207,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
 #endif
     // A wave's records of chunk ch: rec32[gofs, gofs + ne), ne a multiple of 4; bounds in slot ch & 3
     auto chunk_range = [&](int64_t ch, int &gofs, int &ne) {
-        const int32_t *bb = bnd + (ch & 3) * 64;
+        const int32_t *bb = bnd + (ch & (SD_BR - 1)) * 64;
         gofs = __builtin_amdgcn_readfirstlane(bb[wave]);
         ne = __builtin_amdgcn_readfirstlane(bb[wave + 1]) - gofs;
 #ifdef SD_PROF
@@ -1129,7 +1226,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     // data has landed (nor is a scalar load in flight while the compiler counts its own LDS reads
     // with lgkmcnt); the first window of a chunk puts the copy wait and the barrier in between,
     // which hides its load latency.
-    typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+    typedef sd_u32x8 u32x8;
     u32x8 r0, r1, r2, r3, r4, r5;
 #define SD_LOADS                                                                                     \
     "s_load_dwordx8 %0, %6, 0x0\n\t"                                                                  \
@@ -1138,9 +1235,9 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     "s_load_dwordx8 %3, %6, 0x60\n\t"                                                                 \
     "s_load_dwordx8 %4, %6, 0x80\n\t"                                                                 \
     "s_load_dwordx8 %5, %6, 0xa0\n\t"
-    // walk of chunk ch (panel in buffer ch & 1); the first window is in r0 .. r5
+    // walk of chunk ch (panel in buffer ch % SD_NB); the first window is in r0 .. r5
     auto walk_chunk = [&](int64_t ch, int gofs, int ne) {
-        const uint32_t L = lanebase + (uint32_t)((ch & 1) * G::PANEL_B);
+        const uint32_t L = lanebase + (uint32_t)((ch & (SD_NB - 1)) * G::PANEL_B);
         auto walk = [&](const uint32_t (&wr)[SD_SW], int nw) {
             static_assert(SU_D == 4, "one sd_add4 per step");
             auto rec = [&](int x) -> uint32_t { return x < SD_SW ? wr[x < SD_SW ? x : 0] : G::PAD; };
@@ -1196,25 +1293,46 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
         }
     };
 
+    // Copy slot s (s < nchunks): the record bounds of chunk s + 1 (wave 0; clamped at the last
+    // chunk, so every slot has the same instruction count) and the panel of chunk s. Slot s is
+    // issued SD_PD chunks ahead of its walk, into the buffer chunk s - SD_NB last used.
+    auto issue_slot = [&](int64_t s) {
+        dma_bounds(s + 1 < nchunks ? s + 1 : nchunks - 1);
+#ifndef SD_ABLATE_COPY   // diagnostic build: no copies
+        dma_panel(s);
+#endif
+    };
     dma_bounds(0);
-    if (nchunks > 1) dma_bounds(1);
-    if (nchunks > 0) dma_panel(0);
     wait_vm<0>();
     __syncthreads();
     int gofs = 0, ne = 0;
     if (nchunks > 0) chunk_range(0, gofs, ne);
+    for (int64_t s = 0; s < SD_PD && s < nchunks; ++s) issue_slot(s);
+#ifdef SD_ABLATE_REC   // diagnostic build: every chunk walks chunk 0's first window (valid records)
+    asm volatile(SD_LOADS "s_waitcnt lgkmcnt(0)"
+                 : "=&s"(r0), "=&s"(r1), "=&s"(r2), "=&s"(r3), "=&s"(r4), "=&s"(r5)
+                 : "s"(rec32 + gofs)
+                 : "memory");
+#endif
+#ifdef SD_ABLATE_COPY
+    constexpr int NIW = 0;
+#else
+    constexpr int NIW = NI;
+#endif
     for (int64_t ch = 0; ch < nchunks; ++ch) {
-        asm volatile(SD_LOADS "s_waitcnt vmcnt(0)\n\ts_barrier\n\ts_waitcnt lgkmcnt(0)"
-                     : "=&s"(r0), "=&s"(r1), "=&s"(r2), "=&s"(r3), "=&s"(r4), "=&s"(r5)
-                     : "s"(rec32 + gofs)
-                     : "memory");
+        // this wave's copies of slot ch (panel ch, bounds ch + 1) have landed once at most the
+        // slots issued after it are in flight (in-order vmcnt), then the barrier makes every
+        // wave's copies visible; the last SD_PD - 1 chunks wait for everything
+        if (ch + SD_PD - 1 < nchunks) {
+            if (wave == 0) sd_top<(SD_PD - 1) * (NIW + 1)>(r0, r1, r2, r3, r4, r5, rec32 + gofs);
+            else sd_top<(SD_PD - 1) * NIW>(r0, r1, r2, r3, r4, r5, rec32 + gofs);
+        } else {
+            sd_top<0>(r0, r1, r2, r3, r4, r5, rec32 + gofs);
+        }
         SD_T(1);
         const int gofs_c = gofs, ne_c = ne;
         if (ch + 1 < nchunks) chunk_range(ch + 1, gofs, ne);   // bounds ch + 1: visible since this barrier
-        if (ch + 2 < nchunks) dma_bounds(ch + 2);
-#ifndef SD_ABLATE_COPY   // diagnostic build: no copies
-        if (ch + 1 < nchunks) dma_panel(ch + 1);
-#endif
+        if (ch + SD_PD < nchunks) issue_slot(ch + SD_PD);
         SD_T(2);
         walk_chunk(ch, gofs_c, ne_c);
     }
@@ -1366,9 +1484,9 @@ __global__ void place_kernel(int64_t nnz, const int64_t *rows, const int64_t *co
 // hipErrorNotSupported (nothing done): too many records for int32 offsets.
 static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, const int64_t *rows, const int64_t *cols,
                                  const double *vals, int64_t nnz, bool y_k, hipStream_t s) {
-    static_assert(SD_KC == 128, "kcs and mask words below");
+    static_assert(SD_KC >= 32, "whole mask words per virtual row");
     SparseApply p = p0;
-    p.kcs = 7;                           // log2(SD_KC)
+    p.kcs = SD_KCS;
     const int mw = SD_KC / 32;           // mask words per virtual row
     const int64_t nchunks = p.K > 0 ? (p.K + SD_KC - 1) / SD_KC : 0;
     const int64_t NV = nchunks * p.M;
@@ -1437,8 +1555,18 @@ static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, co
         const int64_t nrb_u = (p.M + SU_ROWS - 1) / SU_ROWS;
         const dim3 grid_u((unsigned)(((p.N + SU_J - 1) / SU_J) * nrb_u));
         const int vec_out = p.crs == 1 && (p.ccs % 2) == 0 && (((uintptr_t)p.C) % 16) == 0;
-        if (y_k) hipLaunchKernelGGL((saso_dma_kernel<false>), grid_u, dim3(SU_NT), 0, s, p, seg, rec, nchunks, nrb_u, vec_out);
-        else hipLaunchKernelGGL((saso_dma_kernel<true>), grid_u, dim3(SU_NT), 0, s, p, seg, rec, nchunks, nrb_u, vec_out);
+        // buffer-resource copies when a column tile (64 columns to K) spans less than 2^31 bytes
+        const bool buf = y_k && ((int64_t)SU_J * p.ysj + p.K) * (int64_t)sizeof(double) < ((int64_t)1 << 31);
+#ifdef SD_NO_BUF   // diagnostic build: global-address copies only
+        const bool use_buf = false;
+#else
+        const bool use_buf = buf;
+#endif
+        if (y_k && use_buf)
+            hipLaunchKernelGGL((saso_dma_kernel<false, true>), grid_u, dim3(SU_NT), 0, s, p, seg, rec, nchunks, nrb_u, vec_out);
+        else if (y_k)
+            hipLaunchKernelGGL((saso_dma_kernel<false, false>), grid_u, dim3(SU_NT), 0, s, p, seg, rec, nchunks, nrb_u, vec_out);
+        else hipLaunchKernelGGL((saso_dma_kernel<true, false>), grid_u, dim3(SU_NT), 0, s, p, seg, rec, nchunks, nrb_u, vec_out);
         err = hipGetLastError();
         timing_end(s);
     }
@@ -1464,6 +1592,9 @@ static bool dma_eligible(const SparseApply &p, bool &y_k) {
     constexpr int VEC = 2;
     y_k = p.ysk == 1 && (p.ysj % VEC) == 0 && (((uintptr_t)p.Y) % 16) == 0 && (p.K % VEC) == 0;
     const bool y_jd = p.ysj == 1 && (p.ysk % VEC) == 0 && (((uintptr_t)p.Y) % 16) == 0 && (p.N % VEC) == 0;
+#ifdef SD_NO_DMA   // diagnostic build: the register-staged unit kernel takes these calls
+    return false;
+#endif
     return p.unit_vals && (p.alpha == 1.0 || p.alpha == -1.0) && (y_k || y_jd);
 }
 

@@ -137,7 +137,9 @@ def test_lskges_apply_shapes(cuda, layout, opA, dtype, d, n, m, vec):
 @pytest.mark.parametrize("d,n,m,vec,major", [(1000, 130, 2048, 8, "S"),   # ragged rows; 130 columns
                                              (512, 64, 1024, 20, "S"),    # ~80 records per wave per chunk
                                              (200, 72, 999, 3, "L"),      # LASO, K not a chunk multiple
-                                             (33, 8, 300, 2, "S")])       # one partial row block
+                                             (33, 8, 300, 2, "S"),        # one partial row block
+                                             (40, 16, 100, 2, "S"),       # fewer chunks than panels in flight
+                                             (24, 64, 64, 3, "S")])       # a single chunk
 def test_lskges_unit_alpha_shapes(cuda, layout, opS, opA, dtype, alpha, beta, d, n, m, vec, major):
     """Sampled operators with |alpha| = 1 (the uniform-value kernel with c = 1): bitwise against the
     oracle, including dense chunks (multi-window waves), LASO and ragged shapes."""
