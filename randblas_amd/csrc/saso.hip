@@ -919,6 +919,12 @@ constexpr int SD_KC = 1 << SD_KCS;   // contracted indices per chunk
 constexpr int SD_NB = SD_NB_DEF;     // panel buffers (a ring)
 constexpr int SD_PD = SD_PD_DEF;     // panels in flight ahead of the walked one
 static_assert(SD_NB >= SD_PD + 1 && (SD_NB & (SD_NB - 1)) == 0, "ring: the walked panel plus the ones in flight");
+#ifndef SD_PAD8_DEF
+#define SD_PAD8_DEF 1
+#endif
+// Y along k: SD_PAD8 pads each panel column by 8 B (stride KC * 8 + 8) instead of XOR-swizzling
+// its 16-B slots, so the 32 lanes of a ds_read_b64 lane group hit 64 distinct banks
+constexpr bool SD_PAD8 = SD_PAD8_DEF;
 constexpr int SD_BR = 8;             // record-bound ring slots (chunks c + 1 .. c + SD_PD + 1 live)
 static_assert(SD_BR >= SD_PD + 2, "bounds ring");
 constexpr int SD_SW = 48;    // records per scalar-load window (C3: 0.708 ms with 32, 0.692 ms with 48)
@@ -926,7 +932,8 @@ constexpr int SD_SW = 48;    // records per scalar-load window (C3: 0.708 ms wit
 struct SdCfg {
     typedef double T;
     static constexpr int VEC = 16 / (int)sizeof(T);
-    static constexpr int PANEL_B = SD_KC * SU_J * (int)sizeof(T);   // bytes per panel buffer
+    static constexpr int CSTR = SD_KC * (int)sizeof(T) + (SD_PAD8 ? 8 : 0);   // column stride (Y along k)
+    static constexpr int PANEL_B = SU_J * CSTR;                     // bytes per panel buffer
     static constexpr int BND_OFF = SD_NB * PANEL_B;                 // record bounds: a ring of SD_BR chunks
     static constexpr int MAIN_B = BND_OFF + SD_BR * 64 * 4;
     static constexpr int EPI_B = SuCfg<T>::EPI * (int)sizeof(T);
@@ -948,7 +955,7 @@ struct SdAcc {
 // followed by its M0 wait state (section 4). LDS reads of the walk stay in flight across the
 // section: index mode relocates the VGPR operands of VALU instructions, not memory returns.
 // The wait state after each index write is an SALU instruction that does useful work: the shift
-// that extracts a later batch's panel offsets (kn[q] = wn[q] >> 8; index mode does not touch SALU).
+// that extracts a later batch's panel offsets (kn[q] = bits 8-27 of wn[q]; index mode does not touch SALU).
 // Against an s_nop there: C3 kernel 0.620 -> 0.612 ms (same box, three alternations).
 __device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t *w, const double *y, uint32_t sgn,
                                         const uint32_t *wn, uint32_t *kn) {
@@ -972,16 +979,16 @@ __device__ __forceinline__ void sd_add4(SdAcc &acc, const uint32_t *w, const dou
 #pragma unroll
     for (int q = 0; q < 4; ++q) ys[q] = __builtin_bit_cast(double, (yb[q] & 0xffffffffull) | ((uint64_t)hi[q] << 32));
     asm volatile("s_set_gpr_idx_on %7, gpr_idx(SRC0,DST)\n\t"
-                 "s_lshr_b32 %3, %15, 8\n\t"
+                 "s_bfe_u32 %3, %15, 0x140008\n\t"
                  "v_add_f64 v[32:33], v[32:33], %11\n\t"
                  "s_set_gpr_idx_idx %8\n\t"
-                 "s_lshr_b32 %4, %16, 8\n\t"
+                 "s_bfe_u32 %4, %16, 0x140008\n\t"
                  "v_add_f64 v[32:33], v[32:33], %12\n\t"
                  "s_set_gpr_idx_idx %9\n\t"
-                 "s_lshr_b32 %5, %17, 8\n\t"
+                 "s_bfe_u32 %5, %17, 0x140008\n\t"
                  "v_add_f64 v[32:33], v[32:33], %13\n\t"
                  "s_set_gpr_idx_idx %10\n\t"
-                 "s_lshr_b32 %6, %18, 8\n\t"
+                 "s_bfe_u32 %6, %18, 0x140008\n\t"
                  "v_add_f64 v[32:33], v[32:33], %14\n\t"
                  "s_set_gpr_idx_off"
                  : "+{v[32:63]}"(acc.a), "+{v[64:95]}"(acc.b), "+{v[96:97]}"(acc.dmy),
@@ -1143,6 +1150,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     // are not stored)
     constexpr int NI = KC * SU_J * (int)sizeof(T) / 1024 / 16;
     static_assert(NI >= 1, "whole instructions per wave");
+    static_assert(!SD_PAD8 || KC * (int)sizeof(T) == 1024, "padded columns: one column per copy instruction");
     // BUF (Y along k, the launcher checked that 64 columns + K fit 32-bit byte offsets): the copies
     // go through a buffer resource based at the column tile, per-lane offsets precomputed (columns
     // past N clamped to the last one); a chunk that runs past K takes the clamped global form below
@@ -1160,7 +1168,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
             constexpr int COLB = KC * (int)sizeof(T), CPI = 1024 / COLB, SPC = COLB / 16;
             const int inst = wave * NI + i;
             const int col = inst * CPI + (int)lane / SPC;
-            const int v = ((int)lane % SPC) ^ (col & 15);
+            const int v = SD_PAD8 ? (int)lane % SPC : ((int)lane % SPC) ^ (col & 15);
             const int64_t cj = col < jl ? col : jl - 1;
             bvoff[i] = (uint32_t)((cj * p.ysj + VEC * v) * (int64_t)sizeof(T));
         }
@@ -1171,7 +1179,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
         if (BUF && kc0 + KC <= p.K) {
             const uint32_t soff = (uint32_t)(kc0 * (int64_t)sizeof(T));
 #pragma unroll
-            for (int i = 0; i < NI; ++i) dma16_buf(rsrc, bvoff[i], soff, pb + (uint32_t)((wave * NI + i) * 1024));
+            for (int i = 0; i < NI; ++i) dma16_buf(rsrc, bvoff[i], soff, pb + (uint32_t)((wave * NI + i) * (SD_PAD8 ? G::CSTR : 1024)));
             return;
         }
 #pragma unroll
@@ -1182,10 +1190,10 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
                 constexpr int CPI = 1024 / COLB;            // columns per instruction
                 constexpr int SPC = COLB / 16;              // 16-B slots per column
                 const int col = inst * CPI + (int)lane / SPC;
-                const int v = ((int)lane % SPC) ^ (col & 15);
+                const int v = SD_PAD8 ? (int)lane % SPC : ((int)lane % SPC) ^ (col & 15);
                 const int64_t gj = j0 + col < p.N ? j0 + col : p.N - 1;
                 const int64_t gk = kc0 + VEC * v < p.K ? kc0 + VEC * v : 0;
-                dma16(Y + gj * p.ysj + gk, pb + (uint32_t)(inst * 1024));
+                dma16(Y + gj * p.ysj + gk, pb + (uint32_t)(inst * (SD_PAD8 ? G::CSTR : 1024)));
             } else {
                 constexpr int RB = SU_J * (int)sizeof(T);   // bytes per panel row
                 constexpr int RPI = 1024 / RB;              // rows per instruction
@@ -1200,7 +1208,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     uint32_t sgn = 0x80000000u;   // the sign-bit mask, kept in a VGPR for the walk's bitop3
     asm volatile("" : "+v"(sgn));
     const uint32_t lanebase = YJ ? lane * (uint32_t)sizeof(T)
-                                 : lane * (uint32_t)(KC * sizeof(T)) + 16u * (lane & 15u);
+                                 : (SD_PAD8 ? lane * (uint32_t)G::CSTR : lane * (uint32_t)(KC * sizeof(T)) + 16u * (lane & 15u));
 #ifdef SD_PROF
     uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t pf_t = clock64();
@@ -1247,7 +1255,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
 #pragma unroll
                 for (int q = 0; q < SU_D; ++q) {
                     w[q] = rec(x0 + q);
-                    y[q] = *reinterpret_cast<const T *>(lbase + (L ^ (kf[q] & 0xfffffu)));
+                    y[q] = *reinterpret_cast<const T *>(lbase + (SD_PAD8 ? L + kf[q] : L ^ kf[q]));
                 }
             };
             auto update = [&](const T (&y)[SU_D], const uint32_t (&w)[SU_D], int xn, uint32_t (&kn)[SU_D]) {
@@ -1259,7 +1267,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
             T ya[SU_D], yb[SU_D];
             uint32_t wa[SU_D], wb[SU_D], ka[SU_D], kb[SU_D];
 #pragma unroll
-            for (int q = 0; q < SU_D; ++q) { ka[q] = rec(q) >> 8; kb[q] = rec(SU_D + q) >> 8; }
+            for (int q = 0; q < SU_D; ++q) { ka[q] = (rec(q) >> 8) & 0xfffffu; kb[q] = (rec(SU_D + q) >> 8) & 0xfffffu; }
             issue(0, ya, wa, ka);
             const int nsteps = (nw + SU_D - 1) / SU_D;
             // straight-line walk (a window has at most SD_SW entries): no loop-carried wait state;
