@@ -892,18 +892,26 @@ __global__ __launch_bounds__(SU_NT) void saso_unit_kernel(const SparseApply p, c
 //    copies of panel ch and bounds ch + 1 and meet the other waves at a barrier (every copy for
 //    chunk ch is in LDS; chunk ch - 1 is walked, its buffer free) -> read bounds ch + 1 -> issue
 //    bounds ch + 2 and panel ch + 1 -> walk chunk ch.
-//    Panel layouts, unpadded; the walk address is lane_base ^ koff:
-//      * Y contiguous along k (YJ = false): [64 columns][KC]; 16-B vector v of column c sits in
-//        slot v ^ (c & 15), which spreads the 64 lanes' reads of one k over the banks;
-//        koff = k * sizeof(T).
+//    The copies are issued by the first SD_CW = 4 waves only (one per SIMD, 16 instructions each):
+//    an LDS-DMA instruction holds its wave for hundreds of cycles while the CU's copy path drains,
+//    and with every wave copying every wave started its walk that late; with four copying waves
+//    the other twelve walk at once (C3 kernel 0.61 -> 0.57 ms; 8 waves 0.58, 2 waves 0.81, copies
+//    spread through the copying waves' walks 0.59-0.61).
+//    Panel layouts; the walk address is lane_base + koff (lane_base ^ koff unpadded):
+//      * Y contiguous along k (YJ = false): [64 columns][KC], column stride KC * 8 + 8 B (SD_PAD8:
+//        32 lanes reading one k then cover all 64 banks; the XOR swizzle of 16-B slots it
+//        replaces left a 2-way conflict); koff = k * sizeof(T). The copies reach these 8-B
+//        aligned bases through a buffer resource (BUF: per-lane offsets fixed, the chunk's k offset
+//        in soffset, no address arithmetic per chunk).
 //      * Y contiguous along j (YJ = true): [KC][64 columns]; koff = k * 64 * sizeof(T).
 //    Records: one contiguous segment per (chunk, wave's 32 rows), padded to a multiple of four with
 //    padding records, which add into a dummy accumulator register (v[96:97]); read with scalar
 //    loads (s_load_dwordx8 x 6) straight into SGPRs, SD_SW = 48 per window, so an entry costs
 //    three VALU (address, sign, add) and three SALU ops and no readlane.
-//    Measured on C3 and kept out: 64-deep chunks with 2, 3 or 4 panels,
-//    a flag ring instead of the barrier, a rotating or dedicated copy wave, copies interleaved
-//    with the walk, an L2 prefetch of the panel after next.
+//    Measured on C3 and kept out: 64-deep chunks with 2, 3 or 4 panels
+//    (also as a ring with 2-3 panels in flight: 0.72 ms), a flag ring instead of the barrier, a
+//    rotating or dedicated copy wave, copies interleaved with the walk, an L2 prefetch of the
+//    panel after next.
 // ------------------------------------------------------------------------------------------
 #ifndef SD_KCS_DEF
 #define SD_KCS_DEF 7
@@ -925,6 +933,16 @@ static_assert(SD_NB >= SD_PD + 1 && (SD_NB & (SD_NB - 1)) == 0, "ring: the walke
 // Y along k: SD_PAD8 pads each panel column by 8 B (stride KC * 8 + 8) instead of XOR-swizzling
 // its 16-B slots, so the 32 lanes of a ds_read_b64 lane group hit 64 distinct banks
 constexpr bool SD_PAD8 = SD_PAD8_DEF;
+#ifndef SD_CW_DEF
+#define SD_CW_DEF 4
+#endif
+constexpr int SD_CW = SD_CW_DEF;   // waves that issue the panel copies (the first SD_CW)
+#ifndef SD_CWI_D0
+#define SD_CWI_D0 0   // > 0: a copying wave issues this many copies before its walk ...
+#endif
+#ifndef SD_CWI_DPS
+#define SD_CWI_DPS 2  // ... then this many after each walk step, the rest after the walk
+#endif
 constexpr int SD_BR = 8;             // record-bound ring slots (chunks c + 1 .. c + SD_PD + 1 live)
 static_assert(SD_BR >= SD_PD + 2, "bounds ring");
 constexpr int SD_SW = 48;    // records per scalar-load window (C3: 0.708 ms with 32, 0.692 ms with 48)
@@ -1148,8 +1166,9 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     // panel of chunk cc -> buffer cc & 1; 1 KB per instruction, NI per wave; out-of-range sources
     // clamped (the elements they bring are never read: no record points at k >= K, columns >= N
     // are not stored)
-    constexpr int NI = KC * SU_J * (int)sizeof(T) / 1024 / 16;
-    static_assert(NI >= 1, "whole instructions per wave");
+    constexpr int NI = KC * SU_J * (int)sizeof(T) / 1024 / SD_CW;   // copy instructions per copying wave
+    static_assert(NI >= 1 && NI * SD_CW * 1024 == KC * SU_J * (int)sizeof(T), "whole instructions per wave");
+    static_assert(SD_CW == 16 || SD_PD == 1, "vmcnt counts assume every wave copies");
     static_assert(!SD_PAD8 || KC * (int)sizeof(T) == 1024, "padded columns: one column per copy instruction");
     // BUF (Y along k, the launcher checked that 64 columns + K fit 32-bit byte offsets): the copies
     // go through a buffer resource based at the column tile, per-lane offsets precomputed (columns
@@ -1174,6 +1193,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
         }
     }
     auto dma_panel = [&](int64_t cc) {
+        if (SD_CW < 16 && wave >= SD_CW) return;
         const uint32_t pb = lds0 + (uint32_t)((cc & (SD_NB - 1)) * G::PANEL_B);
         const int64_t kc0 = cc * KC;
         if (BUF && kc0 + KC <= p.K) {
@@ -1205,6 +1225,12 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
         }
     };
 
+    // copy instruction i (compile-time after unrolling) of panel cc in the buffer-resource form
+    auto dma_one = [&](int64_t cc, int i) {
+        const uint32_t pb = lds0 + (uint32_t)((cc & (SD_NB - 1)) * G::PANEL_B);
+        dma16_buf(rsrc, bvoff[i], (uint32_t)(cc * KC * (int64_t)sizeof(T)),
+                  pb + (uint32_t)((wave * NI + i) * (SD_PAD8 ? G::CSTR : 1024)));
+    };
     uint32_t sgn = 0x80000000u;   // the sign-bit mask, kept in a VGPR for the walk's bitop3
     asm volatile("" : "+v"(sgn));
     const uint32_t lanebase = YJ ? lane * (uint32_t)sizeof(T)
@@ -1244,9 +1270,20 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     "s_load_dwordx8 %4, %6, 0x80\n\t"                                                                 \
     "s_load_dwordx8 %5, %6, 0xa0\n\t"
     // walk of chunk ch (panel in buffer ch % SD_NB); the first window is in r0 .. r5
-    auto walk_chunk = [&](int64_t ch, int gofs, int ne) {
+    auto walk_chunk = [&](int64_t ch, int gofs, int ne, bool inter) {
         const uint32_t L = lanebase + (uint32_t)((ch & (SD_NB - 1)) * G::PANEL_B);
-        auto walk = [&](const uint32_t (&wr)[SD_SW], int nw) {
+        // interleaved copies of panel ch + 1 (SD_CWI_D0 > 0, copying waves): after walk step st of
+        // the first window
+        auto hook = [&](int st, bool first) {
+            if (SD_CWI_D0 > 0 && first && inter) {
+#pragma unroll
+                for (int d = 0; d < SD_CWI_DPS; ++d) {
+                    const int i = SD_CWI_D0 + st * SD_CWI_DPS + d;
+                    if (i < NI) dma_one(ch + 1, i < NI ? i : 0);
+                }
+            }
+        };
+        auto walk = [&](const uint32_t (&wr)[SD_SW], int nw, bool first) {
             static_assert(SU_D == 4, "one sd_add4 per step");
             auto rec = [&](int x) -> uint32_t { return x < SD_SW ? wr[x < SD_SW ? x : 0] : G::PAD; };
             // records of step x0 / SU_D into w; their panel offsets kf (record >> 8) come from the
@@ -1278,9 +1315,11 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
                 if (s2 >= nsteps) break;
                 issue((s2 + 1) * SU_D, yb, wb, kb);
                 update(ya, wa, (s2 + 2) * SU_D, ka);
+                hook(s2, first);
                 if (s2 + 1 >= nsteps) break;
                 issue((s2 + 2) * SU_D, ya, wa, ka);
                 update(yb, wb, (s2 + 3) * SU_D, kb);
+                hook(s2 + 1, first);
             }
         };
         for (int done = 0; done < ne; done += SD_SW) {
@@ -1296,7 +1335,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
                 wr[q] = r0[q]; wr[8 + q] = r1[q]; wr[16 + q] = r2[q];
                 wr[24 + q] = r3[q]; wr[32 + q] = r4[q]; wr[40 + q] = r5[q];
             }
-            walk(wr, ne - done < SD_SW ? ne - done : SD_SW);
+            walk(wr, ne - done < SD_SW ? ne - done : SD_SW, done == 0);
             SD_T(5);
         }
     };
@@ -1340,9 +1379,26 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
         SD_T(1);
         const int gofs_c = gofs, ne_c = ne;
         if (ch + 1 < nchunks) chunk_range(ch + 1, gofs, ne);   // bounds ch + 1: visible since this barrier
-        if (ch + SD_PD < nchunks) issue_slot(ch + SD_PD);
+        // interleaved copies (SD_CWI_D0 > 0): a copying wave issues the first SD_CWI_D0 copies of
+        // panel ch + 1 here, more after each step of its walk, the rest after it
+        const bool inter = SD_CWI_D0 > 0 && SD_PD == 1 && BUF && wave < SD_CW && ch + 1 < nchunks &&
+                           (ch + 1) * KC + KC <= p.K;
+        if (inter) {
+            dma_bounds(ch + 2 < nchunks ? ch + 2 : nchunks - 1);
+#pragma unroll
+            for (int i = 0; i < (SD_CWI_D0 < NI ? SD_CWI_D0 : NI); ++i) dma_one(ch + 1, i);
+        } else if (ch + SD_PD < nchunks) {
+            issue_slot(ch + SD_PD);
+        }
         SD_T(2);
-        walk_chunk(ch, gofs_c, ne_c);
+        walk_chunk(ch, gofs_c, ne_c, inter);
+        if (inter) {
+            const int st = ne_c <= 0 ? 0 : ((ne_c < SD_SW ? ne_c : SD_SW) + SU_D - 1) / SU_D;
+            const int issued = SD_CWI_D0 + SD_CWI_DPS * st;
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+                if (i >= issued) dma_one(ch + 1, i);
+        }
     }
 #undef SD_LOADS
 #ifdef SD_PROF
