@@ -909,9 +909,10 @@ __global__ __launch_bounds__(SU_NT) void saso_unit_kernel(const SparseApply p, c
 //    loads (s_load_dwordx8 x 6) straight into SGPRs, SD_SW = 48 per window, so an entry costs
 //    three VALU (address, sign, add) and three SALU ops and no readlane.
 //    Measured on C3 and kept out: 64-deep chunks with 2, 3 or 4 panels
-//    (also as a ring with 2-3 panels in flight: 0.72 ms), a flag ring instead of the barrier, a
-//    rotating or dedicated copy wave, copies interleaved with the walk, an L2 prefetch of the
-//    panel after next.
+//    (also as a ring with 2-3 panels in flight: 0.72 ms), a ring of five half-chunk slots filling
+//    all 160 KiB (96 KiB in flight, bounds by scalar load: 0.59 against 0.57 ms), a flag ring
+//    instead of the barrier, a rotating or dedicated copy wave, copies interleaved with the walk,
+//    an L2 prefetch of the panel after next.
 // ------------------------------------------------------------------------------------------
 #ifndef SD_KCS_DEF
 #define SD_KCS_DEF 7
@@ -937,12 +938,6 @@ constexpr bool SD_PAD8 = SD_PAD8_DEF;
 #define SD_CW_DEF 4
 #endif
 constexpr int SD_CW = SD_CW_DEF;   // waves that issue the panel copies (the first SD_CW)
-#ifndef SD_CWI_D0
-#define SD_CWI_D0 0   // > 0: a copying wave issues this many copies before its walk ...
-#endif
-#ifndef SD_CWI_DPS
-#define SD_CWI_DPS 2  // ... then this many after each walk step, the rest after the walk
-#endif
 constexpr int SD_BR = 8;             // record-bound ring slots (chunks c + 1 .. c + SD_PD + 1 live)
 static_assert(SD_BR >= SD_PD + 2, "bounds ring");
 constexpr int SD_SW = 48;    // records per scalar-load window (C3: 0.708 ms with 32, 0.692 ms with 48)
@@ -1104,7 +1099,7 @@ __device__ __forceinline__ void sd_top(sd_u32x8 &r0, sd_u32x8 &r1, sd_u32x8 &r2,
 // Diagnostic build only (-DSD_PROF, tools/build_var.sh + tools/saso_prof.py): per-phase cycle
 // totals of the DMA apply, summed over waves: 1 record load + barrier, 2 copy issue, 3 bounds,
 // 4 later record windows, 5 walk; 6 entries, 7 wave-chunks.
-__device__ unsigned long long rbh_sd_prof[8];
+__device__ unsigned long long rbh_sd_prof[16];   // [0, 8): copying waves, [8, 16): the others
 #define SD_T(slot) do { const uint64_t now_ = clock64(); pf[slot] += now_ - pf_t; pf_t = now_; } while (0)
 #else
 #define SD_T(slot) do { } while (0)
@@ -1225,12 +1220,6 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
         }
     };
 
-    // copy instruction i (compile-time after unrolling) of panel cc in the buffer-resource form
-    auto dma_one = [&](int64_t cc, int i) {
-        const uint32_t pb = lds0 + (uint32_t)((cc & (SD_NB - 1)) * G::PANEL_B);
-        dma16_buf(rsrc, bvoff[i], (uint32_t)(cc * KC * (int64_t)sizeof(T)),
-                  pb + (uint32_t)((wave * NI + i) * (SD_PAD8 ? G::CSTR : 1024)));
-    };
     uint32_t sgn = 0x80000000u;   // the sign-bit mask, kept in a VGPR for the walk's bitop3
     asm volatile("" : "+v"(sgn));
     const uint32_t lanebase = YJ ? lane * (uint32_t)sizeof(T)
@@ -1270,20 +1259,9 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     "s_load_dwordx8 %4, %6, 0x80\n\t"                                                                 \
     "s_load_dwordx8 %5, %6, 0xa0\n\t"
     // walk of chunk ch (panel in buffer ch % SD_NB); the first window is in r0 .. r5
-    auto walk_chunk = [&](int64_t ch, int gofs, int ne, bool inter) {
+    auto walk_chunk = [&](int64_t ch, int gofs, int ne) {
         const uint32_t L = lanebase + (uint32_t)((ch & (SD_NB - 1)) * G::PANEL_B);
-        // interleaved copies of panel ch + 1 (SD_CWI_D0 > 0, copying waves): after walk step st of
-        // the first window
-        auto hook = [&](int st, bool first) {
-            if (SD_CWI_D0 > 0 && first && inter) {
-#pragma unroll
-                for (int d = 0; d < SD_CWI_DPS; ++d) {
-                    const int i = SD_CWI_D0 + st * SD_CWI_DPS + d;
-                    if (i < NI) dma_one(ch + 1, i < NI ? i : 0);
-                }
-            }
-        };
-        auto walk = [&](const uint32_t (&wr)[SD_SW], int nw, bool first) {
+        auto walk = [&](const uint32_t (&wr)[SD_SW], int nw) {
             static_assert(SU_D == 4, "one sd_add4 per step");
             auto rec = [&](int x) -> uint32_t { return x < SD_SW ? wr[x < SD_SW ? x : 0] : G::PAD; };
             // records of step x0 / SU_D into w; their panel offsets kf (record >> 8) come from the
@@ -1315,11 +1293,9 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
                 if (s2 >= nsteps) break;
                 issue((s2 + 1) * SU_D, yb, wb, kb);
                 update(ya, wa, (s2 + 2) * SU_D, ka);
-                hook(s2, first);
                 if (s2 + 1 >= nsteps) break;
                 issue((s2 + 2) * SU_D, ya, wa, ka);
                 update(yb, wb, (s2 + 3) * SU_D, kb);
-                hook(s2 + 1, first);
             }
         };
         for (int done = 0; done < ne; done += SD_SW) {
@@ -1335,7 +1311,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
                 wr[q] = r0[q]; wr[8 + q] = r1[q]; wr[16 + q] = r2[q];
                 wr[24 + q] = r3[q]; wr[32 + q] = r4[q]; wr[40 + q] = r5[q];
             }
-            walk(wr, ne - done < SD_SW ? ne - done : SD_SW, done == 0);
+            walk(wr, ne - done < SD_SW ? ne - done : SD_SW);
             SD_T(5);
         }
     };
@@ -1379,31 +1355,14 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
         SD_T(1);
         const int gofs_c = gofs, ne_c = ne;
         if (ch + 1 < nchunks) chunk_range(ch + 1, gofs, ne);   // bounds ch + 1: visible since this barrier
-        // interleaved copies (SD_CWI_D0 > 0): a copying wave issues the first SD_CWI_D0 copies of
-        // panel ch + 1 here, more after each step of its walk, the rest after it
-        const bool inter = SD_CWI_D0 > 0 && SD_PD == 1 && BUF && wave < SD_CW && ch + 1 < nchunks &&
-                           (ch + 1) * KC + KC <= p.K;
-        if (inter) {
-            dma_bounds(ch + 2 < nchunks ? ch + 2 : nchunks - 1);
-#pragma unroll
-            for (int i = 0; i < (SD_CWI_D0 < NI ? SD_CWI_D0 : NI); ++i) dma_one(ch + 1, i);
-        } else if (ch + SD_PD < nchunks) {
-            issue_slot(ch + SD_PD);
-        }
+        if (ch + SD_PD < nchunks) issue_slot(ch + SD_PD);
         SD_T(2);
-        walk_chunk(ch, gofs_c, ne_c, inter);
-        if (inter) {
-            const int st = ne_c <= 0 ? 0 : ((ne_c < SD_SW ? ne_c : SD_SW) + SU_D - 1) / SU_D;
-            const int issued = SD_CWI_D0 + SD_CWI_DPS * st;
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-                if (i >= issued) dma_one(ch + 1, i);
-        }
+        walk_chunk(ch, gofs_c, ne_c);
     }
 #undef SD_LOADS
 #ifdef SD_PROF
     if (lane == 0)
-        for (int q = 0; q < 8; ++q) atomicAdd(&rbh_sd_prof[q], (unsigned long long)pf[q]);
+        for (int q = 0; q < 8; ++q) atomicAdd(&rbh_sd_prof[q + (wave < SD_CW ? 0 : 8)], (unsigned long long)pf[q]);
 #endif
     wait_vm<0>();
     __syncthreads();   // the epilogue reuses the panel memory
@@ -1641,9 +1600,9 @@ static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, co
 #ifdef SD_PROF
 extern "C" int rbh_diag_saso_prof(unsigned long long *out, int reset) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rbh_sd_prof), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rbh_sd_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long z[16] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(rbh_sd_prof), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;

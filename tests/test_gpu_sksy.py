@@ -195,11 +195,16 @@ def test_sketch_symmetric_triangle_vs_oracle(cuda):
 @pytest.mark.parametrize("layout", ["C", "R"])
 @pytest.mark.parametrize("uplo", ["U", "L"])
 @pytest.mark.parametrize("fmt", ["F", "P"])
-@pytest.mark.parametrize("n", [600, 2560])
-def test_sksy_tri_full_and_packed(cuda, side, layout, uplo, fmt, n):
+@pytest.mark.parametrize("n,mat", [(600, False), (2560, False), (2560, True)])
+def test_sksy_tri_full_and_packed(cuda, side, layout, uplo, fmt, n, mat, monkeypatch):
     """rbh_sksy_tri: only triangle uplo is read (the other holds NaN), beta != 0, full or packed.
     n = 2560 spans five 512-row memory tiles (every tile class of the one-triangle kernel: inside
-    the triangle, mirrored and straddling the diagonal, several times per output tile)."""
+    the triangle, mirrored and straddling the diagonal, several times per output tile); with mat
+    the operator window is materialised first (RBH_MATERIALISE=1, the kernels' GMAT form)."""
+    if mat:
+        monkeypatch.setenv("RBH_MATERIALISE", "1")
+    else:
+        monkeypatch.delenv("RBH_MATERIALISE", raising=False)
     d = 80
     M = sym_full(n, 6)
     br, bc = (d, n) if side == "L" else (n, d)

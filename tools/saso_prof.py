@@ -17,7 +17,7 @@ S = rb.SparseSkOp(rb.SparseDist(d, m, 8), rb.RNGState(0))
 out = torch.empty(d * n, dtype=torch.float64, device=dev)
 fn = rb.lib.rbh_diag_saso_prof
 fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-buf = (ctypes.c_ulonglong * 8)()
+buf = (ctypes.c_ulonglong * 16)()
 for it in range(4):
     rb.sketch_general_left("C", "N", "N", d, n, m, 1.0, S, A, m, 0.0, out, d)
     torch.cuda.synchronize()
@@ -25,7 +25,8 @@ for it in range(4):
     if it == 0:
         continue
     names = ["(unused)", "record load + barrier", "copy issue", "bounds", "later windows", "walk"]
-    tot = sum(buf[q] for q in range(6))
-    wc = buf[7]
-    print(f"iter {it}: wave-chunks {wc}, entries/wave-chunk {buf[6] / max(wc, 1):.2f}, cycles/wave-chunk {tot / max(wc, 1):.0f}")
-    print("   " + ", ".join(f"{nm} {buf[q] / max(wc, 1):.0f} ({100.0 * buf[q] / max(tot, 1):.1f}%)" for q, nm in enumerate(names)))
+    for grp, o in (("copying waves", 0), ("other waves", 8)):
+        tot = sum(buf[o + q] for q in range(6))
+        wc = buf[o + 7]
+        print(f"iter {it} {grp}: wave-chunks {wc}, entries/wave-chunk {buf[o + 6] / max(wc, 1):.2f}, cycles/wave-chunk {tot / max(wc, 1):.0f}")
+        print("   " + ", ".join(f"{nm} {buf[o + q] / max(wc, 1):.0f} ({100.0 * buf[o + q] / max(tot, 1):.1f}%)" for q, nm in enumerate(names)))
