@@ -213,6 +213,9 @@ def main():
     ap.add_argument("--dry-run", action="store_true", help="launch/report path only, no device work (CPU, gloo)")
     ap.add_argument("--lda-pad", type=int, default=0,
                     help="diagnostics: store the dense A with leading dimension m + pad (same matrix)")
+    ap.add_argument("--dist", action="store_true",
+                    help="run the sharded drivers through an RCCL process group even at N = 1 (the one-GPU "
+                         "rehearsal of the multi-GPU path: all-gather + HIP unpack inside the step)")
     ap.add_argument("--split-d", action="store_true",
                     help="fixed problem (strong scaling): the config's total d split over the ranks (ro_s = g d / N)")
     args = ap.parse_args()
@@ -228,8 +231,13 @@ def main():
     if args.dry_run:
         dry_run(args, world, rank)
         return
-    if world > 1:
+    use_dist = world > 1 or args.dist
+    if use_dist:
         torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -295,7 +303,7 @@ def main():
         timed(lambda: rb.sketch_symmetric_tri("C", "L", "U", "P", d, n, 1.0, S, A, 0, 0.0, out, d, ro_s=ro_s), record)
 
     recording = [False]
-    if world > 1 and kind == "saso":
+    if use_dist and kind == "saso":
         from randblas_amd.distributed import ColumnShardedSketch
 
         B_full = torch.empty(d * world * n, dtype=tdt, device=dev)
@@ -305,7 +313,7 @@ def main():
         def step(record=False):
             recording[0] = record
             drv(B_full)
-    elif world > 1:
+    elif use_dist:
         from randblas_amd.distributed import RowShardedSketch
 
         B_full = torch.empty(d_total * n, dtype=tdt, device=dev)
@@ -334,7 +342,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     rb.kernel_timing(True)   # HIP events around each call's dominant kernel, on its launch stream
@@ -342,11 +350,11 @@ def main():
     for _ in range(args.steps):
         step(record=True)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if use_dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -414,13 +422,13 @@ def main():
                        "symmetry_check": ("tol=0, timed in the step" if kind == "sksy" else None),
                        "A_storage": {"sksy": "full", "sksyp": "packed upper (n(n+1)/2)"}.get(kind, "full"),
                        "parallelism": (f"{'column' if kind == 'saso' else 'row'}-shard x{world} + RCCL all-gather"
-                                       if world > 1 else "single GPU")},
+                                       if use_dist else "single GPU")},
             "pct_of_peak": roof["frac"] * 100.0,
             "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

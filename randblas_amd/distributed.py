@@ -18,6 +18,9 @@ draw the S tiles they need exactly as the unchunked call's tiles would.
 The per-shard compute is a callable so the same driver runs the HIP path (bench.py) and the CPU
 oracle (tests/test_distributed_cpu.py):  compute(ro_s, j0, j1, out)  writes the d_loc x (j1-j0)
 ColMajor shard  B[ro_s : ro_s + d_loc, j0 : j1]  into the 1-D tensor `out`.
+
+The all-gather runs whenever a process group is initialised, a group of one included: that is how
+the one-GPU box drives RCCL together with the HIP path (tests/test_gpu_rccl.py).
 """
 from __future__ import annotations
 
@@ -44,8 +47,9 @@ class RowShardedSketch:
     def __init__(self, d_total: int, n: int, compute: Callable[[int, int, int, torch.Tensor], None],
                  dtype: torch.dtype, device: torch.device, chunks: int = 4, group=None):
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.dist = dist.is_initialized()   # gather through the group (RCCL / gloo), even a group of one
+        self.world = dist.get_world_size(group) if self.dist else 1
+        self.rank = dist.get_rank(group) if self.dist else 0
         if d_total % self.world:
             raise ValueError(f"d_total={d_total} is not divisible by the world size {self.world}")
         self.d_total, self.n = d_total, n
@@ -68,7 +72,7 @@ class RowShardedSketch:
         works: List = []
         for c, (j0, j1) in enumerate(self.cols):
             self.compute(self.ro_s, j0, j1, self.local[c])
-            if self.world > 1 and B_full is not None:
+            if self.dist and B_full is not None:
                 works.append(dist.all_gather_into_tensor(self.gathered[c], self.local[c], group=self.group,
                                                          async_op=True))
         if B_full is None:
@@ -76,9 +80,9 @@ class RowShardedSketch:
         for c, (j0, j1) in enumerate(self.cols):
             nc = j1 - j0
             # ColMajor d_total x n: column j of rank g's shard lands at j * d_total + g * d_loc
-            if self.world > 1:
+            if self.dist:
                 works[c].wait()
-            src = self.gathered[c] if self.world > 1 else self.local[c]
+            src = self.gathered[c] if self.dist else self.local[c]
             _unpack(src, self.world, nc, self.d_loc, B_full[j0 * self.d_total:], self.d_total, self.d_loc)
 
 
@@ -96,8 +100,9 @@ class ColumnShardedSketch:
     def __init__(self, d: int, n_loc: int, compute: Callable[[int, int, torch.Tensor], None],
                  dtype: torch.dtype, device: torch.device, chunks: int = 4, group=None):
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.dist = dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.dist else 1
+        self.rank = dist.get_rank(group) if self.dist else 0
         self.d, self.n_loc = d, n_loc
         self.compute = compute
         self.chunks = max(1, min(chunks, n_loc))
@@ -118,7 +123,7 @@ class ColumnShardedSketch:
         works: List = []
         for c, (j0, j1) in enumerate(self.cols):
             self.compute(j0, j1, self.local[c])
-            if self.world > 1 and B_full is not None:
+            if self.dist and B_full is not None:
                 works.append(dist.all_gather_into_tensor(self.gathered[c], self.local[c], group=self.group,
                                                          async_op=True))
         if B_full is None:
@@ -126,7 +131,7 @@ class ColumnShardedSketch:
         for c, (j0, j1) in enumerate(self.cols):
             nc = j1 - j0
             # [rank][local column][row]: rank g's column j0 + j at (g n_loc + j0 + j) d
-            if self.world > 1:
+            if self.dist:
                 works[c].wait()
-            src = self.gathered[c] if self.world > 1 else self.local[c]
+            src = self.gathered[c] if self.dist else self.local[c]
             _unpack(src, self.world, nc, self.d, B_full[j0 * self.d:], self.d, self.n_loc * self.d)

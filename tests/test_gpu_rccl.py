@@ -1,0 +1,47 @@
+"""The multi-GPU path on one GPU: an RCCL (torch "nccl" backend) process group of one, launched by
+torch.distributed.run exactly as the driver launches N ranks, runs the sharded drivers with the HIP
+path -- all_gather_into_tensor over RCCL, then the HIP unpack (randblas_amd/distributed.py) -- and
+bench.py --dist times that step. Each launcher is a child process (never an exec)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _torchrun(args, timeout=110):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.gpu
+def test_sharded_drivers_over_rccl_bitwise():
+    r = _torchrun([os.path.join("tests", "rccl_worker.py")])
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "rccl_worker: ok" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config", ["c1", "c3"])
+def test_bench_dist_step_over_rccl(config):
+    """bench.py --dist: the timed step includes the RCCL all-gather and the unpack; one JSON line."""
+    r = _torchrun(["bench.py", "--gpus", "1", "--dist", "--config", config, "--steps", "2", "--warmup", "1",
+                   "--no-cpu-baseline"])
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 1 and "RCCL all-gather" in line["config"]["parallelism"]
+    assert line["value"] > 0 and line["kernel_launches_per_step"] >= 1
