@@ -245,7 +245,6 @@ def main():
     kind, dtype, d, m, n, vec_nnz = CONFIGS[args.config]
     d_total, d, scaling = shard_rows(args, world)   # d: this rank's rows (dense) / all rows (SASO)
     tdt = torch.float64 if dtype == "f64" else torch.float32
-    stream = torch.cuda.current_stream(dev)
 
     # A ~ DenseDist(m, n) Gaussian key 99, ColMajor, generated on the device (input, not timed).
     # SASO shards by columns: rank g holds columns [g n, (g+1) n) of DenseDist(m, world n).
@@ -280,9 +279,10 @@ def main():
             return
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
+        st = torch.cuda.current_stream(dev)   # the sharded drivers run chunks on their own streams
+        e0.record(st)
         fn()
-        e1.record(stream)
+        e1.record(st)
         k_ev.append((e0, e1))
 
     def compute(ro_s, j0, j1, out, record=False):
@@ -366,20 +366,27 @@ def main():
     ms_step = elapsed * 1e3 / args.steps
     cols_per_launch = n * args.steps / max(launches, 1)
 
-    # roofline of the dominant kernel: algorithmic work of one launch / its average duration
+    # roofline of the dominant kernel: algorithmic work of one launch / its average duration. With
+    # the sharded drivers (N > 1 or --dist) two chunk kernels run at once on two streams, so a
+    # launch's duration is shared; there the roofline is this rank's work per step / the step time
     esz = 8 if dtype == "f64" else 4
+    per = "step" if use_dist else "kernel"
+    t_s = (ms_step if use_dist else kern_ms) * 1e-3
+    if use_dist:
+        cols_per_launch = n
     if kind == "saso":
         alg = (m * cols_per_launch + d * cols_per_launch) * esz   # read A panel once, write B once
-        achieved = alg / (kern_ms * 1e-3)
+        achieved = alg / t_s
         roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK, "traffic": None}
     else:
         flops = 2.0 * d * m * cols_per_launch
-        achieved = flops / (kern_ms * 1e-3)
+        achieved = flops / t_s
         roof = {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK[dtype] / 1e12, "unit": "TFLOP/s",
                 "frac": achieved / PEAK[dtype], "traffic": None}
 
-    if world == 1:
+    roof["basis"] = per
+    if not use_dist:
         roof["traffic"], roof["traffic_source"] = pmc_traffic(args.config)
 
     cpu = None

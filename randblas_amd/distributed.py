@@ -21,6 +21,11 @@ ColMajor shard  B[ro_s : ro_s + d_loc, j0 : j1]  into the 1-D tensor `out`.
 
 The all-gather runs whenever a process group is initialised, a group of one included: that is how
 the one-GPU box drives RCCL together with the HIP path (tests/test_gpu_rccl.py).
+
+On the GPU the chunks are computed on two streams in turn. A chunk's grid is a fraction of the
+unchunked call's (C2: 128 workgroups of 512 for a quarter of the columns, on 256 CUs), so one chunk
+at a time would leave CUs idle; two in flight fill the chip, and each chunk's all-gather starts as
+soon as its own kernel ends.
 """
 from __future__ import annotations
 
@@ -28,6 +33,30 @@ from typing import Callable, List, Optional
 
 import torch
 import torch.distributed as dist
+
+
+class _Streams:
+    """Compute streams for the chunks (CUDA tensors; None on CPU): chunk c runs on stream c % 2,
+    after whatever the caller's stream has queued (the previous step's unpack and gather waits)."""
+
+    def __init__(self, device: torch.device, n: int = 2):
+        self.main = None
+        self.s = [torch.cuda.Stream(device) for _ in range(n)] if device.type == "cuda" else []
+
+    def begin(self):
+        if self.s:
+            self.main = torch.cuda.current_stream(self.s[0].device)
+            for st in self.s:
+                st.wait_stream(self.main)
+
+    def ctx(self, c: int):
+        import contextlib
+        return torch.cuda.stream(self.s[c % len(self.s)]) if self.s else contextlib.nullcontext()
+
+    def end(self):
+        if self.s:
+            for st in self.s:
+                self.main.wait_stream(st)
 
 
 def _unpack(src: torch.Tensor, nshards: int, rows: int, run: int, dst: torch.Tensor, row_stride: int,
@@ -61,6 +90,7 @@ class RowShardedSketch:
         self.local = [torch.empty(self.d_loc * (j1 - j0), dtype=dtype, device=device) for j0, j1 in self.cols]
         self.gathered = [torch.empty(self.world * self.d_loc * (j1 - j0), dtype=dtype, device=device)
                          for j0, j1 in self.cols]
+        self.streams = _Streams(torch.device(device))
 
     @property
     def ro_s(self) -> int:
@@ -70,11 +100,14 @@ class RowShardedSketch:
         """Compute this rank's shard; if B_full (ColMajor d_total x n, 1-D) is given, reassemble the
         whole sketch into it on every rank."""
         works: List = []
+        self.streams.begin()
         for c, (j0, j1) in enumerate(self.cols):
-            self.compute(self.ro_s, j0, j1, self.local[c])
-            if self.dist and B_full is not None:
-                works.append(dist.all_gather_into_tensor(self.gathered[c], self.local[c], group=self.group,
-                                                         async_op=True))
+            with self.streams.ctx(c):   # the gather waits for this chunk's stream only
+                self.compute(self.ro_s, j0, j1, self.local[c])
+                if self.dist and B_full is not None:
+                    works.append(dist.all_gather_into_tensor(self.gathered[c], self.local[c], group=self.group,
+                                                             async_op=True))
+        self.streams.end()
         if B_full is None:
             return
         for c, (j0, j1) in enumerate(self.cols):
@@ -111,6 +144,7 @@ class ColumnShardedSketch:
         self.local = [torch.empty(d * (j1 - j0), dtype=dtype, device=device) for j0, j1 in self.cols]
         self.gathered = [torch.empty(self.world * d * (j1 - j0), dtype=dtype, device=device)
                          for j0, j1 in self.cols]
+        self.streams = _Streams(torch.device(device))
 
     @property
     def co(self) -> int:
@@ -121,11 +155,14 @@ class ColumnShardedSketch:
         """Compute this rank's columns; if B_full (ColMajor d x world*n_loc, 1-D) is given, gather the
         whole sketch into it on every rank."""
         works: List = []
+        self.streams.begin()
         for c, (j0, j1) in enumerate(self.cols):
-            self.compute(j0, j1, self.local[c])
-            if self.dist and B_full is not None:
-                works.append(dist.all_gather_into_tensor(self.gathered[c], self.local[c], group=self.group,
-                                                         async_op=True))
+            with self.streams.ctx(c):
+                self.compute(j0, j1, self.local[c])
+                if self.dist and B_full is not None:
+                    works.append(dist.all_gather_into_tensor(self.gathered[c], self.local[c], group=self.group,
+                                                             async_op=True))
+        self.streams.end()
         if B_full is None:
             return
         for c, (j0, j1) in enumerate(self.cols):
