@@ -341,6 +341,8 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    if use_dist:
+        drv.streams.timing = True   # compute vs exposed exchange per timed step
     torch.cuda.synchronize()
     if use_dist:
         dist.barrier()
@@ -359,6 +361,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     call_ms = float(np.sum([a.elapsed_time(b) for a, b in k_ev])) / args.steps   # library time per step
+    comp_ms, exch_ms = drv.streams.split_ms() if use_dist else (None, None)
     kt = rb.kernel_times_ms()
     rb.kernel_timing(False)
     launches = len(kt)
@@ -409,6 +412,10 @@ def main():
             "kernel_ms": kern_ms,
             "kernel_launches_per_step": launches / args.steps,
             "library_ms_per_step": call_ms,
+            # sharded runs (rank 0): chunk compute (both streams joined) and the all-gather + unpack
+            # left exposed after it, per step
+            "compute_ms_per_step": comp_ms,
+            "exposed_exchange_ms_per_step": exch_ms,
             "higher_is_better": True,
             "scaling": scaling,
             "vs_baseline": None,

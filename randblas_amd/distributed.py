@@ -37,15 +37,27 @@ import torch.distributed as dist
 
 class _Streams:
     """Compute streams for the chunks (CUDA tensors; None on CPU): chunk c runs on stream c % 2,
-    after whatever the caller's stream has queued (the previous step's unpack and gather waits)."""
+    after whatever the caller's stream has queued (the previous step's unpack and gather waits).
+    With timing on, every call records three events on the caller's stream: start, compute done
+    (both streams joined), and done (every chunk gathered and unpacked), so a caller can split a
+    step into compute and the exchange that is left exposed after it."""
 
     def __init__(self, device: torch.device, n: int = 2):
         self.main = None
         self.s = [torch.cuda.Stream(device) for _ in range(n)] if device.type == "cuda" else []
+        self.timing = False
+        self.marks: List = []   # (start, compute done, done) per call
+
+    def _event(self):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(self.main)
+        return e
 
     def begin(self):
         if self.s:
             self.main = torch.cuda.current_stream(self.s[0].device)
+            if self.timing:
+                self.marks.append([self._event()])
             for st in self.s:
                 st.wait_stream(self.main)
 
@@ -57,6 +69,20 @@ class _Streams:
         if self.s:
             for st in self.s:
                 self.main.wait_stream(st)
+            if self.timing:
+                self.marks[-1].append(self._event())
+
+    def done(self):
+        if self.s and self.timing:
+            self.marks[-1].append(self._event())
+
+    def split_ms(self):
+        """Mean (compute, exposed exchange) milliseconds per timed call (after a synchronize)."""
+        if not self.marks:
+            return None, None
+        comp = sum(a.elapsed_time(b) for a, b, _ in self.marks) / len(self.marks)
+        exch = sum(b.elapsed_time(c) for _, b, c in self.marks) / len(self.marks)
+        return comp, exch
 
 
 def _unpack(src: torch.Tensor, nshards: int, rows: int, run: int, dst: torch.Tensor, row_stride: int,
@@ -117,6 +143,7 @@ class RowShardedSketch:
                 works[c].wait()
             src = self.gathered[c] if self.dist else self.local[c]
             _unpack(src, self.world, nc, self.d_loc, B_full[j0 * self.d_total:], self.d_total, self.d_loc)
+        self.streams.done()
 
 
 class ColumnShardedSketch:
@@ -172,3 +199,4 @@ class ColumnShardedSketch:
                 works[c].wait()
             src = self.gathered[c] if self.dist else self.local[c]
             _unpack(src, self.world, nc, self.d, B_full[j0 * self.d:], self.d, self.n_loc * self.d)
+        self.streams.done()
