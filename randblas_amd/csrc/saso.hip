@@ -938,14 +938,6 @@ constexpr bool SD_PAD8 = SD_PAD8_DEF;
 #define SD_CW_DEF 4
 #endif
 constexpr int SD_CW = SD_CW_DEF;   // waves that issue the panel copies (the first SD_CW)
-#ifndef SD_H3_DEF
-#define SD_H3_DEF 0
-#endif
-// SD_H3 (Y along k, full-size buffer-resource copies): the first SD_H3C columns of a panel get a
-// ring of three buffers, filled two chunks ahead, the other columns the usual two: 64 + 26 KiB in
-// flight instead of 64 in the same 160 KiB
-constexpr bool SD_H3 = SD_H3_DEF;
-constexpr int SD_H3C = 24;
 constexpr int SD_BR = 8;             // record-bound ring slots (chunks c + 1 .. c + SD_PD + 1 live)
 static_assert(SD_BR >= SD_PD + 2, "bounds ring");
 constexpr int SD_SW = 48;    // records per scalar-load window (C3: 0.708 ms with 32, 0.692 ms with 48)
@@ -956,12 +948,7 @@ struct SdCfg {
     static constexpr int CSTR = SD_KC * (int)sizeof(T) + (SD_PAD8 ? 8 : 0);   // column stride (Y along k)
     static constexpr int PANEL_B = SU_J * CSTR;                     // bytes per panel buffer
     static constexpr int BND_OFF = SD_NB * PANEL_B;                 // record bounds: a ring of SD_BR chunks
-    static constexpr int MAIN_B0 = BND_OFF + SD_BR * 64 * 4;
-    // SD_H3 layout: [3 x SD_H3C columns][2 x (64 - SD_H3C) columns][bounds]
-    static constexpr int H3A_SLOT = SD_H3C * CSTR, H3B_SLOT = (SU_J - SD_H3C) * CSTR;
-    static constexpr int H3B_OFF = 3 * H3A_SLOT, H3_BND = H3B_OFF + 2 * H3B_SLOT;
-    static constexpr int MAIN_B1 = H3_BND + SD_BR * 64 * 4;
-    static constexpr int MAIN_B = SD_H3 && MAIN_B1 > MAIN_B0 ? MAIN_B1 : MAIN_B0;
+    static constexpr int MAIN_B = BND_OFF + SD_BR * 64 * 4;
     static constexpr int EPI_B = SuCfg<T>::EPI * (int)sizeof(T);
     static constexpr int BYTES = MAIN_B > EPI_B ? MAIN_B : EPI_B;
     static constexpr uint32_t PAD = 64u;   // padding record: the dummy's register index, koff 0, sign +
@@ -1129,9 +1116,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     __shared__ __attribute__((aligned(16))) char smem[G::BYTES];
     const char *lbase = smem;
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
-    constexpr bool H3 = SD_H3 && !YJ && BUF;
-    constexpr int BNDO = H3 ? G::H3_BND : G::BND_OFF;
-    const int32_t *bnd = reinterpret_cast<const int32_t *>(smem + BNDO);
+    const int32_t *bnd = reinterpret_cast<const int32_t *>(smem + G::BND_OFF);
 
     const int tid = threadIdx.x;
     const uint32_t lane = tid & 63;
@@ -1170,7 +1155,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
         if (wave == 0) {
             const int64_t l = lane < 16 ? lane : 16;
             const int64_t g = grp0 + l < NG ? grp0 + l : NG;
-            dma4(seg + cc * NG + g, lds0 + BNDO + (uint32_t)((cc & (SD_BR - 1)) * 256));
+            dma4(seg + cc * NG + g, lds0 + G::BND_OFF + (uint32_t)((cc & (SD_BR - 1)) * 256));
         }
     };
     // panel of chunk cc -> buffer cc & 1; 1 KB per instruction, NI per wave; out-of-range sources
@@ -1180,12 +1165,6 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     static_assert(NI >= 1 && NI * SD_CW * 1024 == KC * SU_J * (int)sizeof(T), "whole instructions per wave");
     static_assert(SD_CW == 16 || SD_PD == 1, "vmcnt counts assume every wave copies");
     static_assert(!SD_PAD8 || KC * (int)sizeof(T) == 1024, "padded columns: one column per copy instruction");
-    // SD_H3: copying wave w issues columns SD_H3C + w (NI - H3NA) + i of part B, then w H3NA + i' of part A
-    constexpr int H3NA = SD_H3C / SD_CW;
-    static_assert(!H3 || (SD_PAD8 && SD_PD == 1 && SD_NB == 2 && SD_CW * H3NA == SD_H3C), "hybrid ring layout");
-    auto h3_col = [&](int w, int i) -> int {
-        return i < NI - H3NA ? SD_H3C + w * (NI - H3NA) + i : w * H3NA + (i - (NI - H3NA));
-    };
     // BUF (Y along k, the launcher checked that 64 columns + K fit 32-bit byte offsets): the copies
     // go through a buffer resource based at the column tile, per-lane offsets precomputed (columns
     // past N clamped to the last one); a chunk that runs past K takes the clamped global form below
@@ -1202,40 +1181,12 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
         for (int i = 0; i < NI; ++i) {
             constexpr int COLB = KC * (int)sizeof(T), CPI = 1024 / COLB, SPC = COLB / 16;
             const int inst = wave * NI + i;
-            const int col = H3 ? h3_col(wave, i) : inst * CPI + (int)lane / SPC;
+            const int col = inst * CPI + (int)lane / SPC;
             const int v = SD_PAD8 ? (int)lane % SPC : ((int)lane % SPC) ^ (col & 15);
             const int64_t cj = col < jl ? col : jl - 1;
             bvoff[i] = (uint32_t)((cj * p.ysj + VEC * v) * (int64_t)sizeof(T));
         }
     }
-    // SD_H3: LDS byte offset of column col of chunk cc, and the two copy parts: B = columns
-    // SD_H3C..63 of chunk cc (each copying wave's first NI - H3NA instructions), A = columns
-    // 0..SD_H3C-1 (its last H3NA)
-    auto h3_dst = [&](int64_t cc, int col) -> uint32_t {
-        return col < SD_H3C ? (uint32_t)((cc % 3) * G::H3A_SLOT + col * G::CSTR)
-                            : (uint32_t)(G::H3B_OFF + (cc & 1) * G::H3B_SLOT + (col - SD_H3C) * G::CSTR);
-    };
-    auto h3_part = [&](int64_t cc, bool partA) {
-        if (wave >= SD_CW) return;
-        const int64_t kc0 = cc * KC;
-        const bool full = kc0 + KC <= p.K;
-        const uint32_t soff = (uint32_t)(kc0 * (int64_t)sizeof(T));
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            if ((i >= NI - H3NA) != partA) continue;
-            const int col = h3_col(wave, i);
-            const uint32_t dst = lds0 + h3_dst(cc, col);
-            if (full) {
-                dma16_buf(rsrc, bvoff[i], soff, dst);
-            } else {
-                constexpr int SPC = KC * (int)sizeof(T) / 16;
-                const int v = (int)lane % SPC;
-                const int64_t gj = j0 + col < p.N ? j0 + col : p.N - 1;
-                const int64_t gk = kc0 + VEC * v < p.K ? kc0 + VEC * v : 0;
-                dma16(Y + gj * p.ysj + gk, dst);
-            }
-        }
-    };
     auto dma_panel = [&](int64_t cc) {
         if (SD_CW < 16 && wave >= SD_CW) return;
         const uint32_t pb = lds0 + (uint32_t)((cc & (SD_NB - 1)) * G::PANEL_B);
@@ -1309,7 +1260,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     "s_load_dwordx8 %5, %6, 0xa0\n\t"
     // walk of chunk ch (panel in buffer ch % SD_NB); the first window is in r0 .. r5
     auto walk_chunk = [&](int64_t ch, int gofs, int ne) {
-        const uint32_t L = H3 ? h3_dst(ch, (int)lane) : lanebase + (uint32_t)((ch & (SD_NB - 1)) * G::PANEL_B);
+        const uint32_t L = lanebase + (uint32_t)((ch & (SD_NB - 1)) * G::PANEL_B);
         auto walk = [&](const uint32_t (&wr)[SD_SW], int nw) {
             static_assert(SU_D == 4, "one sd_add4 per step");
             auto rec = [&](int x) -> uint32_t { return x < SD_SW ? wr[x < SD_SW ? x : 0] : G::PAD; };
@@ -1379,16 +1330,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     __syncthreads();
     int gofs = 0, ne = 0;
     if (nchunks > 0) chunk_range(0, gofs, ne);
-    if (H3) {   // bounds 1, all of panel 0, part A of panel 1
-        if (nchunks > 0) {
-            dma_bounds(nchunks > 1 ? 1 : 0);
-            h3_part(0, false);
-            h3_part(0, true);
-        }
-        if (nchunks > 1) h3_part(1, true);
-    } else {
-        for (int64_t s = 0; s < SD_PD && s < nchunks; ++s) issue_slot(s);
-    }
+    for (int64_t s = 0; s < SD_PD && s < nchunks; ++s) issue_slot(s);
 #ifdef SD_ABLATE_REC   // diagnostic build: every chunk walks chunk 0's first window (valid records)
     asm volatile(SD_LOADS "s_waitcnt lgkmcnt(0)"
                  : "=&s"(r0), "=&s"(r1), "=&s"(r2), "=&s"(r3), "=&s"(r4), "=&s"(r5)
@@ -1404,12 +1346,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
         // this wave's copies of slot ch (panel ch, bounds ch + 1) have landed once at most the
         // slots issued after it are in flight (in-order vmcnt), then the barrier makes every
         // wave's copies visible; the last SD_PD - 1 chunks wait for everything
-        if (H3) {
-            // H3: this wave's bounds ch + 1 and parts B(ch), A(ch) landed once at most part A of
-            // panel ch + 1 (issued after them) is in flight
-            if (wave < SD_CW && ch + 1 < nchunks) sd_top<H3NA>(r0, r1, r2, r3, r4, r5, rec32 + gofs);
-            else sd_top<0>(r0, r1, r2, r3, r4, r5, rec32 + gofs);
-        } else if (ch + SD_PD - 1 < nchunks) {
+        if (ch + SD_PD - 1 < nchunks) {
             if (wave == 0) sd_top<(SD_PD - 1) * (NIW + 1)>(r0, r1, r2, r3, r4, r5, rec32 + gofs);
             else sd_top<(SD_PD - 1) * NIW>(r0, r1, r2, r3, r4, r5, rec32 + gofs);
         } else {
@@ -1418,15 +1355,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
         SD_T(1);
         const int gofs_c = gofs, ne_c = ne;
         if (ch + 1 < nchunks) chunk_range(ch + 1, gofs, ne);   // bounds ch + 1: visible since this barrier
-        if (H3) {   // bounds ch + 2, part B of panel ch + 1, part A of panel ch + 2
-            if (ch + 1 < nchunks) {
-                dma_bounds(ch + 2 < nchunks ? ch + 2 : nchunks - 1);
-                h3_part(ch + 1, false);
-            }
-            if (ch + 2 < nchunks) h3_part(ch + 2, true);
-        } else if (ch + SD_PD < nchunks) {
-            issue_slot(ch + SD_PD);
-        }
+        if (ch + SD_PD < nchunks) issue_slot(ch + SD_PD);
         SD_T(2);
         walk_chunk(ch, gofs_c, ne_c);
     }
