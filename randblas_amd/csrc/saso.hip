@@ -1061,24 +1061,13 @@ template <int N>
 __device__ __forceinline__ void sd_top(sd_u32x8 &r0, sd_u32x8 &r1, sd_u32x8 &r2, sd_u32x8 &r3, sd_u32x8 &r4,
                                        sd_u32x8 &r5, const uint32_t *rec) {
     static_assert(N >= 0 && N < 64, "vmcnt range");
-#if defined(SD_ABLATE_REC) || defined(SD_ABLATE_BAR)   // diagnostic builds (wrong results, timing only)
-#ifdef SD_ABLATE_REC
-#define SD_REC_ ""
-#else
-#define SD_REC_ "s_load_dwordx8 %0, %6, 0x0\n\ts_load_dwordx8 %1, %6, 0x20\n\ts_load_dwordx8 %2, %6, 0x40\n\t" \
-                "s_load_dwordx8 %3, %6, 0x60\n\ts_load_dwordx8 %4, %6, 0x80\n\ts_load_dwordx8 %5, %6, 0xa0\n\t"
-#endif
-#ifdef SD_ABLATE_BAR
-#define SD_BAR_ ""
-#else
-#define SD_BAR_ "s_barrier\n\t"
-#endif
-    asm volatile(SD_REC_ "s_waitcnt vmcnt(%7)\n\t" SD_BAR_ "s_waitcnt lgkmcnt(0)"
+#ifdef SD_ABLATE_REC   // diagnostic build (wrong results, timing only): no record loads per chunk
+    asm volatile("s_waitcnt vmcnt(%7)\n\t"
+                 "s_barrier\n\t"
+                 "s_waitcnt lgkmcnt(0)"
                  : "+s"(r0), "+s"(r1), "+s"(r2), "+s"(r3), "+s"(r4), "+s"(r5)
                  : "s"(rec), "n"(N)
                  : "memory");
-#undef SD_REC_
-#undef SD_BAR_
 #else
     asm volatile("s_load_dwordx8 %0, %6, 0x0\n\t"
                  "s_load_dwordx8 %1, %6, 0x20\n\t"
