@@ -209,13 +209,18 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--chunks", type=int, default=4, help="column chunks pipelined with the all-gather (N > 1)")
+    ap.add_argument("--chunks", type=int, default=1,
+                    help="column chunks per rank and step, each all-gathered as soon as it is done (N > 1 or --dist; "
+                         "every chunk uses the whole rank problem's split-K, so results do not depend on it)")
     ap.add_argument("--dry-run", action="store_true", help="launch/report path only, no device work (CPU, gloo)")
     ap.add_argument("--lda-pad", type=int, default=0,
                     help="diagnostics: store the dense A with leading dimension m + pad (same matrix)")
     ap.add_argument("--dist", action="store_true",
                     help="run the sharded drivers through an RCCL process group even at N = 1 (the one-GPU "
                          "rehearsal of the multi-GPU path: all-gather + HIP unpack inside the step)")
+    ap.add_argument("--prefilled", action="store_true",
+                    help="SASO: fill the operator once before timing (fill_sparse) and apply it from its arrays in "
+                         "every step, the reference's fill-once / apply-many use; default: sampled in every call")
     ap.add_argument("--split-d", action="store_true",
                     help="fixed problem (strong scaling): the config's total d split over the ranks (ro_s = g d / N)")
     args = ap.parse_args()
@@ -252,6 +257,8 @@ def main():
     if kind == "saso":
         rb.fill_dense("C", rb.DenseDist(m, world * n), m, n, 0, rank * n, A, rb.RNGState(99))
         S = rb.SparseSkOp(rb.SparseDist(d, m, vec_nnz), rb.RNGState(0))
+        if args.prefilled:   # fill once (untimed), apply from the arrays every step (skge.hh:503-504)
+            rb.fill_sparse_op(S)
     else:
         rb.fill_dense("C", rb.DenseDist(m, n), m, n, 0, 0, A, rb.RNGState(99))
         S = rb.DenseSkOp(rb.DenseDist(d_total, m), rb.RNGState(0))
@@ -314,8 +321,9 @@ def main():
             drv = RowShardedSketch(d_total, n, lambda ro, j0, j1, out: fn(ro, out, recording[0]), tdt, dev,
                                    chunks=1)
         else:
-            drv = RowShardedSketch(d_total, n, lambda ro, j0, j1, out: compute(ro, j0, j1, out, recording[0]),
-                                   tdt, dev, chunks=args.chunks)
+            from randblas_amd.distributed import dense_rank_compute
+
+            drv = RowShardedSketch(d_total, n, dense_rank_compute(S, A, lda, m, d, n), tdt, dev, chunks=args.chunks)
 
         def step(record=False):
             recording[0] = record
@@ -334,7 +342,7 @@ def main():
     for _ in range(args.warmup):
         step()
     if use_dist:
-        drv.streams.timing = True   # compute vs exposed exchange per timed step
+        drv.timing = True   # compute per timed step; the rest of the step time is exchange left exposed
     torch.cuda.synchronize()
     if use_dist:
         dist.barrier()
@@ -343,6 +351,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(record=True)
+    if use_dist:
+        drv.wait()   # the last step's exchange (the earlier ones overlapped the next step's compute)
     torch.cuda.synchronize()
     if use_dist:
         dist.barrier()
@@ -352,7 +362,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    comp_ms, exch_ms = drv.streams.split_ms() if use_dist else (None, None)
+    comp_ms = drv.compute_ms() if use_dist else None
     kt = rb.kernel_times_ms()
     rb.kernel_timing(False)
     launches = len(kt)
@@ -360,14 +370,13 @@ def main():
     ms_step = elapsed * 1e3 / args.steps
     cols_per_launch = n * args.steps / max(launches, 1)
 
-    # roofline of the dominant kernel: algorithmic work of one launch / its average duration. With
-    # the sharded drivers (N > 1 or --dist) two chunk kernels run at once on two streams, so a
-    # launch's duration is shared; there the roofline is this rank's work per step / the step time
+    exch_ms = max(0.0, ms_step - comp_ms) if comp_ms is not None else None
+    # roofline of the dominant kernel: algorithmic work of one launch / its average duration (the
+    # sharded drivers run their chunks one after another on the compute stream, so a launch's
+    # events time that launch alone)
     esz = 8 if dtype == "f64" else 4
-    per = "step" if use_dist else "kernel"
-    t_s = (ms_step if use_dist else kern_ms) * 1e-3
-    if use_dist:
-        cols_per_launch = n
+    per = "kernel"
+    t_s = kern_ms * 1e-3
     if kind == "saso":
         alg = (m * cols_per_launch + d * cols_per_launch) * esz   # read A panel once, write B once
         achieved = alg / t_s
@@ -380,8 +389,7 @@ def main():
                 "frac": achieved / PEAK[dtype], "traffic": None}
 
     roof["basis"] = per
-    if not use_dist:
-        roof["traffic"], roof["traffic_source"] = pmc_traffic(args.config)
+    roof["traffic"], roof["traffic_source"] = pmc_traffic(args.config)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -402,8 +410,8 @@ def main():
             "ms_per_step": ms_step,
             "kernel_ms": kern_ms,
             "kernel_launches_per_step": launches / args.steps,
-            # sharded runs (rank 0): chunk compute (both streams joined) and the all-gather + unpack
-            # left exposed after it, per step
+            # sharded runs (rank 0): the compute of a step, and the rest of the step time: the
+            # all-gather + unpack not hidden under the next step's compute
             "compute_ms_per_step": comp_ms,
             "exposed_exchange_ms_per_step": exch_ms,
             "higher_is_better": True,
@@ -411,7 +419,8 @@ def main():
             "vs_baseline": None,
             "dtype": dtype,
             "data": ("synthetic (A ~ Gaussian DenseDist(m,n) key 99 generated on device; "
-                     + ("the SASO operator sampled in every call)" if kind == "saso" else
+                     + (("the SASO operator filled once before timing, applied from its arrays)" if args.prefilled
+                         else "the SASO operator sampled in every call)") if kind == "saso" else
                         "the operator window drawn on the device in every call)")),
             "config": {"workload": {"c1": "Gaussian skge fp64 d=128 A 4096^2 (BASELINE configs[0], the reference's CPU case)",
                                     "c2": "Gaussian skge fp64 (BASELINE configs[1])",

@@ -17,8 +17,8 @@
 // (hipMalloc) are used in place. Link with -lrandblas_hip.
 //
 // A DenseSkOp whose buff is nullptr is regenerated from its Philox counters inside the fused MFMA
-// GEMM, tile by tile into LDS; it is not written to memory (unless the opt-in environment switch
-// RBH_MATERIALISE=1 asks for the window to be drawn into a workspace first).
+// GEMM, tile by tile into LDS; it is not written to memory (unless the thread's options,
+// ext::ScopedOptions, ask for the window to be drawn into a workspace first).
 // fill_dense(S) and submatrix_as_blackbox still fill a host buffer, as in the reference, after
 // which the operator is applied from it.
 #pragma once
@@ -107,6 +107,24 @@ inline void require(bool cond, const char *text, const char *func) {
 }
 }  // namespace detail
 #define RBH_CXX_REQUIRE(c) ::RandBLAS::detail::require((c), #c, __func__)
+
+// Extension (no reference counterpart): execution options for the dense sketches this thread makes
+// through this header (rbh_options of the C ABI: split-K policy, materialised operator window, the
+// one-triangle read of sketch_symmetric). The reference's overloads have no slot for them, so they
+// are per thread and scoped:  { RandBLAS::ext::ScopedOptions o({0, 1, 0, 0}); sketch_general(...); }
+namespace ext {
+inline rbh_options &thread_options() {
+    static thread_local rbh_options o{0, 0, 0, 0};
+    return o;
+}
+struct ScopedOptions {
+    rbh_options saved;
+    explicit ScopedOptions(const rbh_options &o) : saved(thread_options()) { thread_options() = o; }
+    ~ScopedOptions() { thread_options() = saved; }
+    ScopedOptions(const ScopedOptions &) = delete;
+    ScopedOptions &operator=(const ScopedOptions &) = delete;
+};
+}  // namespace ext
 
 enum class MajorAxis : char { Short = 'S', Long = 'L', Undefined = 'U' };
 
@@ -225,8 +243,9 @@ struct DenseSkOp {
         RBH_CXX_REQUIRE(this->dist.n_cols > 0);
         if (dist.family == DenseDistName::BlackBox) RBH_CXX_REQUIRE(this->buff != nullptr);
     }
-    // A copy views the same buffer without owning it; a move takes the ownership along (the
-    // reference's implicit copy would delete an owned buffer twice).
+    // A copy views the same buffer without owning it (so it must not outlive an owning original);
+    // a move takes the ownership along (the reference's implicit copy would delete an owned buffer
+    // twice). Assignment is deleted, as in the reference (its members are const).
     DenseSkOp(const DenseSkOp &o)
         : n_rows(o.n_rows), n_cols(o.n_cols), dist(o.dist), seed_state(o.seed_state), next_state(o.next_state),
           buff(o.buff), layout(o.layout), del_buff_on_destruct(false) {}
@@ -248,15 +267,15 @@ template <> struct Api<double> {
     static int fill_sparse(const rbh_sparse_dist *D, const rbh_state *s, int64_t *r, int64_t *c, double *v) {
         return rbh_fill_sparse_f64(D, s, r, c, v, nullptr);
     }
-    static constexpr auto lskge3 = rbh_lskge3_f64;
-    static constexpr auto rskge3 = rbh_rskge3_f64;
+    static constexpr auto lskge3 = rbh_lskge3_ex_f64;
+    static constexpr auto rskge3 = rbh_rskge3_ex_f64;
     static constexpr auto lskges = rbh_lskges_f64;
     static constexpr auto rskges = rbh_rskges_f64;
     static constexpr auto sym = rbh_require_symmetric_f64;
     static constexpr auto lsksp3 = rbh_lsksp3_f64;
     static constexpr auto rsksp3 = rbh_rsksp3_f64;
-    static constexpr auto sksy = rbh_sketch_symmetric_f64;
-    static constexpr auto sksy_tri = rbh_sksy_tri_f64;
+    static constexpr auto sksy = rbh_sketch_symmetric_ex_f64;
+    static constexpr auto sksy_tri = rbh_sksy_tri_ex_f64;
 };
 template <> struct Api<float> {
     static int fill_dense(char l, const rbh_dense_dist *D, int64_t r, int64_t c, int64_t ro, int64_t co, float *b,
@@ -264,15 +283,15 @@ template <> struct Api<float> {
     static int fill_sparse(const rbh_sparse_dist *D, const rbh_state *s, int64_t *r, int64_t *c, float *v) {
         return rbh_fill_sparse_f32(D, s, r, c, v, nullptr);
     }
-    static constexpr auto lskge3 = rbh_lskge3_f32;
-    static constexpr auto rskge3 = rbh_rskge3_f32;
+    static constexpr auto lskge3 = rbh_lskge3_ex_f32;
+    static constexpr auto rskge3 = rbh_rskge3_ex_f32;
     static constexpr auto lskges = rbh_lskges_f32;
     static constexpr auto rskges = rbh_rskges_f32;
     static constexpr auto sym = rbh_require_symmetric_f32;
     static constexpr auto lsksp3 = rbh_lsksp3_f32;
     static constexpr auto rsksp3 = rbh_rsksp3_f32;
-    static constexpr auto sksy = rbh_sketch_symmetric_f32;
-    static constexpr auto sksy_tri = rbh_sksy_tri_f32;
+    static constexpr auto sksy = rbh_sketch_symmetric_ex_f32;
+    static constexpr auto sksy_tri = rbh_sksy_tri_ex_f32;
 };
 }  // namespace detail
 
@@ -466,7 +485,7 @@ void lsk(blas::Layout layout, blas::Op opS, blas::Op opA, int64_t d, int64_t n, 
     const rbh_dense_dist dd = c_dist(S.dist);
     const rbh_state s = c_state(S.seed_state);
     check(Api<T>::lskge3((char)layout, (char)opS, (char)opA, d, n, m, alpha, &dd, &s, S.buff, (char)S.layout, ro_s,
-                         co_s, A, lda, beta, B, ldb, nullptr));
+                         co_s, A, lda, beta, B, ldb, &ext::thread_options(), nullptr));
 }
 // sparse::lskges / rskges begin with `if (!S.known_filled) fill_sparse(S)` (skge.hh:503-504,
 // :634-635): the caller's operator comes back sampled. When this call did the sampling, the
@@ -493,7 +512,7 @@ void rsk(blas::Layout layout, blas::Op opA, blas::Op opS, int64_t m, int64_t d, 
     const rbh_dense_dist dd = c_dist(S.dist);
     const rbh_state s = c_state(S.seed_state);
     check(Api<T>::rskge3((char)layout, (char)opA, (char)opS, m, d, n, alpha, A, lda, &dd, &s, S.buff,
-                         (char)S.layout, ro_s, co_s, beta, B, ldb, nullptr));
+                         (char)S.layout, ro_s, co_s, beta, B, ldb, &ext::thread_options(), nullptr));
 }
 template <typename T, typename RNG, typename sint_t>
 void rsk(blas::Layout layout, blas::Op opA, blas::Op opS, int64_t m, int64_t d, int64_t n, T alpha, const T *A,
@@ -612,7 +631,7 @@ void sksy(blas::Layout layout, char side, int64_t d, int64_t n, T alpha, DenseSk
     const rbh_dense_dist dd = c_dist(S.dist);
     const rbh_state s = c_state(S.seed_state);
     check(Api<T>::sksy((char)layout, side, d, n, alpha, &dd, &s, S.buff, (char)S.layout, ro_s, co_s, A, lda, beta, B,
-                       ldb, tol, nullptr));
+                       ldb, tol, &ext::thread_options(), nullptr));
 }
 template <typename T, typename RNG, typename sint_t>
 void sksy(blas::Layout layout, char side, int64_t d, int64_t n, T alpha, SparseSkOp<T, RNG, sint_t> &S, int64_t ro_s,
@@ -665,7 +684,8 @@ inline void sketch_symmetric_triangle(blas::Side side, blas::Layout layout, blas
     const rbh_dense_dist dd = c_dist(S.dist);
     const rbh_state s = detail::c_state(S.seed_state);
     detail::check(detail::Api<T>::sksy_tri((char)layout, (char)side, (char)uplo, packed ? 'P' : 'F', d, n, alpha, &dd,
-                                           &s, S.buff, (char)S.layout, ro_s, co_s, A, lda, beta, B, ldb, nullptr));
+                                           &s, S.buff, (char)S.layout, ro_s, co_s, A, lda, beta, B, ldb,
+                                           &ext::thread_options(), nullptr));
 }
 }  // namespace ext
 

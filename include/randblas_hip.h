@@ -67,10 +67,12 @@ int rbh_kernel_timing_collect(float *ms, int max);
 
 /* Workspaces (no reference counterpart): the library keeps the device blocks its calls carve
  * workspaces from, one arena per (device, stream), so repeated calls pay no allocation. This
- * synchronises `stream` and frees its arena's idle blocks; stream == NULL does so for every stream
- * of the current device (call it after destroying streams the library has seen). The library also
- * releases idle blocks by itself before its retained bytes on a device would pass 2 GiB. */
-int rbh_release_workspaces(void *stream);
+ * synchronises `stream` and frees its arena's idle blocks (stream NULL: the null stream's arena);
+ * all_streams != 0 synchronises the device and does so for every stream of the current device (call
+ * it after destroying streams the library has seen). The library also releases idle blocks by
+ * itself before its retained bytes on a device would pass 2 GiB (not while the calling stream is
+ * being captured into a graph). */
+int rbh_release_workspaces(void *stream, int all_streams);
 
 /* Shard reassembly for multi-GPU sketching (no reference counterpart): an
  * all-gather leaves nshards shards one after another, shard g being `rows` runs of `run` elements;
@@ -130,6 +132,100 @@ int rbh_rskge3_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_
                    const float *A, int64_t lda, const rbh_dense_dist *D, const rbh_state *seed,
                    const float *S_buff, char S_layout, int64_t ro_s, int64_t co_s, float beta, float *B,
                    int64_t ldb, void *stream);
+
+/* ---- per-call options and plans (no reference counterpart) ---------------------------------
+ * The _ex entry points take the same arguments as the plain ones plus `opt` (NULL = defaults, which
+ * is what the plain entry points use):
+ *   splitk:        0 = automatic: when the output tiles fill at most half of the device's compute
+ *                  units, K is cut into floor(CUs / tiles) slices whose partial sums a deterministic
+ *                  reduction adds in order (the sum then rounds differently from the unsplit one,
+ *                  within the reference's bound); 1 = never split; s >= 2 = exactly s slices. The
+ *                  slices depend only on (K, s): the columns of a call cut into chunks that all use
+ *                  the same s give the unchunked call's bits (rbh_*_plan reports the automatic s).
+ *   materialise:   1 = draw the operator window into a workspace first, then the GEMM (the
+ *                  reference's fill_dense + gemm shape, bitwise the same result); 0 = draw it inside
+ *                  the GEMM, never storing it (default).
+ *   sksy_triangle: sketch_symmetric only: 1 = when the symmetry check finds A bitwise symmetric,
+ *                  read only its upper triangle (the same bits as full storage);
+ *                  rbh_sketch_symmetric_last_path() then returns 1 (0: full storage was read).
+ *   sparse_filled: sparse sketches with caller COO arrays (rbh_lskges_ex / rbh_rskges_ex): 1 = the
+ *                  arrays are fill_sparse's output for this operator, unmodified. Arrays whose
+ *                  in-window values alpha * v are all +-1 with no repeated (row, k) -- every
+ *                  fill_sparse output applied with |alpha| = 1 -- take the fast LDS-DMA apply after
+ *                  a device check: with 0 (default) the call waits for that check (and falls back to
+ *                  the sorted apply when it fails); with 1 it does not wait, and a failed check
+ *                  makes the sketch NaN. */
+typedef struct rbh_options {
+    int32_t splitk;
+    int32_t materialise;
+    int32_t sksy_triangle;
+    int32_t sparse_filled;
+} rbh_options;
+
+/* The kernel a dense sketch call would launch: kernel 0 none (empty output), 1 beta-scaling only,
+ * 2 generic GEMM, 3 fused GEMM, 4 wide f64 GEMM, 5 wide f32 GEMM (32-deep), 6 wide one-triangle
+ * GEMM, 7 triangle expanded, then the plain kernels; its output tiles, split-K factor and
+ * workgroups (tiles * splitk). */
+typedef struct rbh_plan {
+    int32_t kernel;
+    int32_t splitk;
+    int64_t tiles;
+    int64_t workgroups;
+} rbh_plan;
+
+int rbh_lskge3_ex_f64(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, double alpha,
+                      const rbh_dense_dist *D, const rbh_state *seed, const double *S_buff, char S_layout,
+                      int64_t ro_s, int64_t co_s, const double *A, int64_t lda, double beta, double *B, int64_t ldb,
+                      const rbh_options *opt, void *stream);
+int rbh_lskge3_ex_f32(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, float alpha,
+                      const rbh_dense_dist *D, const rbh_state *seed, const float *S_buff, char S_layout,
+                      int64_t ro_s, int64_t co_s, const float *A, int64_t lda, float beta, float *B, int64_t ldb,
+                      const rbh_options *opt, void *stream);
+int rbh_rskge3_ex_f64(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, double alpha, const double *A,
+                      int64_t lda, const rbh_dense_dist *D, const rbh_state *seed, const double *S_buff, char S_layout,
+                      int64_t ro_s, int64_t co_s, double beta, double *B, int64_t ldb, const rbh_options *opt,
+                      void *stream);
+int rbh_rskge3_ex_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, float alpha, const float *A,
+                      int64_t lda, const rbh_dense_dist *D, const rbh_state *seed, const float *S_buff, char S_layout,
+                      int64_t ro_s, int64_t co_s, float beta, float *B, int64_t ldb, const rbh_options *opt,
+                      void *stream);
+/* The plan of rbh_lskge3 / rbh_rskge3 with these arguments (pointers inspected for alignment only). */
+int rbh_lskge3_plan_f64(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, const rbh_dense_dist *D,
+                        const double *S_buff, char S_layout, int64_t ro_s, int64_t co_s, const double *A, int64_t lda,
+                        int64_t ldb, const rbh_options *opt, rbh_plan *plan);
+int rbh_lskge3_plan_f32(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, const rbh_dense_dist *D,
+                        const float *S_buff, char S_layout, int64_t ro_s, int64_t co_s, const float *A, int64_t lda,
+                        int64_t ldb, const rbh_options *opt, rbh_plan *plan);
+int rbh_rskge3_plan_f64(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, const double *A, int64_t lda,
+                        const rbh_dense_dist *D, const double *S_buff, char S_layout, int64_t ro_s, int64_t co_s,
+                        int64_t ldb, const rbh_options *opt, rbh_plan *plan);
+int rbh_rskge3_plan_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, const float *A, int64_t lda,
+                        const rbh_dense_dist *D, const float *S_buff, char S_layout, int64_t ro_s, int64_t co_s,
+                        int64_t ldb, const rbh_options *opt, rbh_plan *plan);
+
+/* The sparse sketches with per-call options (sparse_filled above). */
+int rbh_lskges_ex_f64(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, double alpha,
+                      const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz, const int64_t *rows,
+                      const int64_t *cols, const double *vals, int64_t ro_s, int64_t co_s, const double *A, int64_t lda,
+                      double beta, double *B, int64_t ldb, const rbh_options *opt, void *stream);
+int rbh_lskges_ex_f32(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, float alpha,
+                      const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz, const int64_t *rows,
+                      const int64_t *cols, const float *vals, int64_t ro_s, int64_t co_s, const float *A, int64_t lda,
+                      float beta, float *B, int64_t ldb, const rbh_options *opt, void *stream);
+int rbh_rskges_ex_f64(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, double alpha, const double *A,
+                      int64_t lda, const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz, const int64_t *rows,
+                      const int64_t *cols, const double *vals, int64_t ro_s, int64_t co_s, double beta, double *B,
+                      int64_t ldb, const rbh_options *opt, void *stream);
+int rbh_rskges_ex_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, float alpha, const float *A,
+                      int64_t lda, const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz, const int64_t *rows,
+                      const int64_t *cols, const float *vals, int64_t ro_s, int64_t co_s, float beta, float *B,
+                      int64_t ldb, const rbh_options *opt, void *stream);
+
+/* Which apply the calling thread's last sparse sketch (or spmm / sketch_sparse) ran: 0 none (empty
+ * output), 1 the LDS-DMA kernel on a sort-free CSR (operators whose values are +-1 after alpha,
+ * without repeated entries), 2 the row gather (very sparse operators), 3 the sorted CSR with the
+ * uniform-value kernel, 4 the sorted CSR with the general kernel. */
+int rbh_sparse_last_path(void);
 
 /* ---- sketch_general, sparse operator ----------------------------------------------------- */
 /* Left: B = alpha * op(submat(S)) * op(A) + beta * B with S a SparseSkOp of D.
@@ -227,8 +323,8 @@ int rbh_spmm_right_f32(char layout, char opA, char opB, int64_t m, int64_t n, in
  * negative), then side 'L': B (d x n) = alpha * submat(S) * A + beta * B (sksy.hh:300-319, 520-537) or
  * side 'R': B (n x d) = alpha * A * submat(S) + beta * B (sksy.hh:165-184, 413-430), submat(S) at
  * (ro_s, co_s) of S ~ D, A n x n full storage in `layout`. RBH_ERR_SYMMETRY when the check fails.
- * (The check also notes whether A is bitwise symmetric; with RBH_SKSY_TRI=1 in the environment
- * only the upper triangle of such an A is read, which gives the same bits.) */
+ * (The check also notes whether A is bitwise symmetric; rbh_sketch_symmetric_ex with
+ * opt->sksy_triangle = 1 then reads only the upper triangle of such an A, which gives the same bits.) */
 int rbh_sketch_symmetric_f64(char layout, char side, int64_t d, int64_t n, double alpha, const rbh_dense_dist *D,
                              const rbh_state *seed, const double *S_buff, char S_layout, int64_t ro_s, int64_t co_s,
                              const double *A, int64_t lda, double beta, double *B, int64_t ldb, double sym_check_tol,
@@ -249,6 +345,25 @@ int rbh_sksy_tri_f32(char layout, char side, char uplo, char A_fmt, int64_t d, i
                      int64_t co_s, const float *A, int64_t lda, float beta, float *B, int64_t ldb, void *stream);
 int rbh_require_symmetric_f64(char layout, const double *A, int64_t n, int64_t lda, double tol, void *stream);
 int rbh_require_symmetric_f32(char layout, const float *A, int64_t n, int64_t lda, float tol, void *stream);
+/* The symmetric entry points with per-call options (rbh_options above). */
+int rbh_sketch_symmetric_ex_f64(char layout, char side, int64_t d, int64_t n, double alpha, const rbh_dense_dist *D,
+                                const rbh_state *seed, const double *S_buff, char S_layout, int64_t ro_s,
+                                int64_t co_s, const double *A, int64_t lda, double beta, double *B, int64_t ldb,
+                                double sym_check_tol, const rbh_options *opt, void *stream);
+int rbh_sketch_symmetric_ex_f32(char layout, char side, int64_t d, int64_t n, float alpha, const rbh_dense_dist *D,
+                                const rbh_state *seed, const float *S_buff, char S_layout, int64_t ro_s,
+                                int64_t co_s, const float *A, int64_t lda, float beta, float *B, int64_t ldb,
+                                float sym_check_tol, const rbh_options *opt, void *stream);
+/* Which storage the calling thread's last successful sketch_symmetric read: 0 full, 1 upper triangle. */
+int rbh_sketch_symmetric_last_path(void);
+int rbh_sksy_tri_ex_f64(char layout, char side, char uplo, char A_fmt, int64_t d, int64_t n, double alpha,
+                        const rbh_dense_dist *D, const rbh_state *seed, const double *S_buff, char S_layout,
+                        int64_t ro_s, int64_t co_s, const double *A, int64_t lda, double beta, double *B, int64_t ldb,
+                        const rbh_options *opt, void *stream);
+int rbh_sksy_tri_ex_f32(char layout, char side, char uplo, char A_fmt, int64_t d, int64_t n, float alpha,
+                        const rbh_dense_dist *D, const rbh_state *seed, const float *S_buff, char S_layout,
+                        int64_t ro_s, int64_t co_s, const float *A, int64_t lda, float beta, float *B, int64_t ldb,
+                        const rbh_options *opt, void *stream);
 
 #ifdef __cplusplus
 }

@@ -55,6 +55,15 @@ class SparseDistC(ctypes.Structure):
     _fields_ = [("n_rows", c_i64), ("n_cols", c_i64), ("vec_nnz", c_i64), ("major_axis", c_char)]
 
 
+class OptionsC(ctypes.Structure):
+    _fields_ = [("splitk", ctypes.c_int32), ("materialise", ctypes.c_int32), ("sksy_triangle", ctypes.c_int32),
+                ("sparse_filled", ctypes.c_int32)]
+
+
+class PlanC(ctypes.Structure):
+    _fields_ = [("kernel", ctypes.c_int32), ("splitk", ctypes.c_int32), ("tiles", c_i64), ("workgroups", c_i64)]
+
+
 class RandBLASError(RuntimeError):
     """RandBLAS::exceptions::Error equivalent (RandBLAS/exceptions.hh:45-70)."""
 
@@ -107,8 +116,25 @@ for _t, _ct in (("f64", ctypes.c_double), ("f32", ctypes.c_float)):
         [c_vp, c_i64, _ct, c_vp, c_i64, c_vp]
     getattr(lib, f"rbh_spmm_right_{_t}").argtypes = [c_char, c_char, c_char, c_i64, c_i64, c_i64, _ct, c_vp, c_i64] + \
         _spm + [_ct, c_vp, c_i64, c_vp]
+    getattr(lib, f"rbh_lskge3_ex_{_t}").argtypes = getattr(lib, f"rbh_lskge3_{_t}").argtypes[:-1] + [P(OptionsC), c_vp]
+    getattr(lib, f"rbh_rskge3_ex_{_t}").argtypes = getattr(lib, f"rbh_rskge3_{_t}").argtypes[:-1] + [P(OptionsC), c_vp]
+    getattr(lib, f"rbh_lskges_ex_{_t}").argtypes = getattr(lib, f"rbh_lskges_{_t}").argtypes[:-1] + [P(OptionsC), c_vp]
+    getattr(lib, f"rbh_rskges_ex_{_t}").argtypes = getattr(lib, f"rbh_rskges_{_t}").argtypes[:-1] + [P(OptionsC), c_vp]
+    getattr(lib, f"rbh_lskge3_plan_{_t}").argtypes = [c_char, c_char, c_char, c_i64, c_i64, c_i64, P(DenseDistC), c_vp,
+                                                      c_char, c_i64, c_i64, c_vp, c_i64, c_i64, P(OptionsC), P(PlanC)]
+    getattr(lib, f"rbh_rskge3_plan_{_t}").argtypes = [c_char, c_char, c_char, c_i64, c_i64, c_i64, c_vp, c_i64,
+                                                      P(DenseDistC), c_vp, c_char, c_i64, c_i64, c_i64, P(OptionsC),
+                                                      P(PlanC)]
 lib.rbh_is_device_pointer.argtypes = [c_vp]
-lib.rbh_release_workspaces.argtypes = [c_vp]
+lib.rbh_release_workspaces.argtypes = [c_vp, ctypes.c_int]
+lib.rbh_sketch_symmetric_last_path.restype = ctypes.c_int
+lib.rbh_sparse_last_path.restype = ctypes.c_int
+SPARSE_PATHS = {0: "none", 1: "dma", 2: "gather", 3: "sorted_unit", 4: "sorted"}
+
+
+def sparse_last_path() -> str:
+    """Which apply this thread's last sparse sketch ran (rbh_sparse_last_path)."""
+    return SPARSE_PATHS[lib.rbh_sparse_last_path()]
 lib.rbh_unpack_shards.argtypes = [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, ctypes.c_int, c_vp]
 for _t, _ct in (("f64", ctypes.c_double), ("f32", ctypes.c_float)):
     getattr(lib, f"rbh_sketch_symmetric_{_t}").argtypes = [c_char, c_char, c_i64, c_i64, _ct, P(DenseDistC),
@@ -117,6 +143,9 @@ for _t, _ct in (("f64", ctypes.c_double), ("f32", ctypes.c_float)):
     getattr(lib, f"rbh_sksy_tri_{_t}").argtypes = [c_char, c_char, c_char, c_char, c_i64, c_i64, _ct, P(DenseDistC),
                                                    P(RNGStateC), c_vp, c_char, c_i64, c_i64, c_vp, c_i64, _ct, c_vp,
                                                    c_i64, c_vp]
+    getattr(lib, f"rbh_sketch_symmetric_ex_{_t}").argtypes = \
+        getattr(lib, f"rbh_sketch_symmetric_{_t}").argtypes[:-1] + [P(OptionsC), c_vp]
+    getattr(lib, f"rbh_sksy_tri_ex_{_t}").argtypes = getattr(lib, f"rbh_sksy_tri_{_t}").argtypes[:-1] + [P(OptionsC), c_vp]
 
 # --------------------------------------------------------------------------------------------
 # Python mirror of the reference's types
@@ -227,6 +256,7 @@ class SparseSkOp:
     cols: object = None
     vals: object = None
     nnz: Optional[int] = None
+    filled_by_library: bool = False   # the arrays are fill_sparse(S)'s own output (set by fill_sparse_op)
 
     @property
     def n_rows(self):
@@ -239,6 +269,43 @@ class SparseSkOp:
     @property
     def next_state(self) -> RNGState:
         return sparse_next_state(self.dist, self.seed_state)
+
+
+@dataclass
+class Options:
+    """Per-call execution options (rbh_options, include/randblas_hip.h): splitk 0 = automatic
+    split-K, 1 = never split, s >= 2 = exactly s slices of K; materialise = draw the operator window
+    into a workspace first; sksy_triangle = sketch_symmetric reads only the upper triangle of a
+    bitwise-symmetric A; sparse_filled = a SparseSkOp's arrays are fill_sparse's unmodified output
+    (the fast apply then does not wait for its device check)."""
+
+    splitk: int = 0
+    materialise: bool = False
+    sksy_triangle: bool = False
+    sparse_filled: bool = False
+
+    def c(self) -> OptionsC:
+        return OptionsC(int(self.splitk), int(bool(self.materialise)), int(bool(self.sksy_triangle)),
+                        int(bool(self.sparse_filled)))
+
+
+PLAN_KERNELS = {0: "none", 1: "scale", 2: "generic", 3: "fused", 4: "wide", 5: "wide32", 6: "wide_tri",
+                7: "symmetrize"}
+
+
+@dataclass
+class Plan:
+    """What a dense sketch call would launch (rbh_plan): kernel name, split-K factor, output tiles,
+    workgroups."""
+
+    kernel: str
+    splitk: int
+    tiles: int
+    workgroups: int
+
+
+def _opt(options):
+    return ctypes.byref(options.c()) if options is not None else None
 
 
 # --------------------------------------------------------------------------------------------
@@ -301,42 +368,99 @@ def fill_sparse(S: SparseSkOp, rows, cols, vals, stream=None) -> None:
               _stream(vals, stream)))
 
 
-def sketch_general_left(layout, opS, opA, d, n, m, alpha, S, A, lda, beta, B, ldb, ro_s=0, co_s=0, stream=None):
-    """B = alpha op(submat(S)) op(A) + beta B (RandBLAS::sketch_general, skge.hh:771-836, 1088-1112)."""
+def _sparse_opts(S, options):
+    """A SparseSkOp whose arrays fill_sparse_op wrote: tell the library (sparse_filled)."""
+    if S.rows is not None and S.filled_by_library:
+        o = options or Options()
+        return Options(o.splitk, o.materialise, o.sksy_triangle, True)
+    return options
+
+
+def fill_sparse_op(S: SparseSkOp, dtype="f64", device=None, stream=None) -> SparseSkOp:
+    """RandBLAS::fill_sparse(S) (sparse_skops.hh:389-413) as the reference does it: S's own COO arrays
+    (device tensors here) are allocated and sampled, and S is marked filled. Later sketches apply S
+    from its arrays -- the reference's fill-once / apply-many use (skge.hh:503-504) -- and, as the
+    arrays are the library's own output, without waiting for the fast apply's device check."""
+    import torch
+
+    device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    nnz = S.dist.nnz
+    tdt = torch.float64 if dtype == "f64" else torch.float32
+    S.rows = torch.empty(nnz, dtype=torch.int64, device=device)
+    S.cols = torch.empty(nnz, dtype=torch.int64, device=device)
+    S.vals = torch.empty(nnz, dtype=tdt, device=device)
+    S.nnz = nnz
+    fill_sparse(S, S.rows, S.cols, S.vals, stream)
+    S.filled_by_library = True
+    return S
+
+
+def sketch_general_left(layout, opS, opA, d, n, m, alpha, S, A, lda, beta, B, ldb, ro_s=0, co_s=0, stream=None,
+                        options: Optional[Options] = None):
+    """B = alpha op(submat(S)) op(A) + beta B (RandBLAS::sketch_general, skge.hh:771-836, 1088-1112).
+    options: per-call Options for a dense operator (rbh_lskge3_ex)."""
     t = _dtype_tag(B)
     st = _stream(B, stream)
     if isinstance(S, DenseSkOp):
-        fn = getattr(lib, f"rbh_lskge3_{t}")
+        fn = getattr(lib, f"rbh_lskge3_ex_{t}")
         _check(fn(_b(layout), _b(opS), _b(opA), d, n, m, alpha, ctypes.byref(S.dist.c()),
                   ctypes.byref(S.seed_state.c()), _ptr(S.buff), _b(S.buff_layout), ro_s, co_s, _ptr(A), lda, beta,
-                  _ptr(B), ldb, st))
+                  _ptr(B), ldb, _opt(options), st))
     elif isinstance(S, SparseSkOp):
-        fn = getattr(lib, f"rbh_lskges_{t}")
+        fn = getattr(lib, f"rbh_lskges_ex_{t}")
         nnz = S.nnz if S.nnz is not None else (S.dist.nnz if S.rows is not None else 0)
         _check(fn(_b(layout), _b(opS), _b(opA), d, n, m, alpha, ctypes.byref(S.dist.c()),
                   ctypes.byref(S.seed_state.c()), nnz, _ptr(S.rows), _ptr(S.cols), _ptr(S.vals), ro_s, co_s, _ptr(A),
-                  lda, beta, _ptr(B), ldb, st))
+                  lda, beta, _ptr(B), ldb, _opt(_sparse_opts(S, options)), st))
     else:
         raise TypeError("S must be a DenseSkOp or SparseSkOp")
 
 
-def sketch_general_right(layout, opA, opS, m, d, n, alpha, A, lda, S, beta, B, ldb, ro_s=0, co_s=0, stream=None):
+def sketch_general_right(layout, opA, opS, m, d, n, alpha, A, lda, S, beta, B, ldb, ro_s=0, co_s=0, stream=None,
+                         options: Optional[Options] = None):
     """B = alpha op(A) op(submat(S)) + beta B (RandBLAS::sketch_general, skge.hh:943-1007, 1190-1214)."""
     t = _dtype_tag(B)
     st = _stream(B, stream)
     if isinstance(S, DenseSkOp):
-        fn = getattr(lib, f"rbh_rskge3_{t}")
+        fn = getattr(lib, f"rbh_rskge3_ex_{t}")
         _check(fn(_b(layout), _b(opA), _b(opS), m, d, n, alpha, _ptr(A), lda, ctypes.byref(S.dist.c()),
                   ctypes.byref(S.seed_state.c()), _ptr(S.buff), _b(S.buff_layout), ro_s, co_s, beta, _ptr(B), ldb,
-                  st))
+                  _opt(options), st))
     elif isinstance(S, SparseSkOp):
-        fn = getattr(lib, f"rbh_rskges_{t}")
+        fn = getattr(lib, f"rbh_rskges_ex_{t}")
         nnz = S.nnz if S.nnz is not None else (S.dist.nnz if S.rows is not None else 0)
         _check(fn(_b(layout), _b(opA), _b(opS), m, d, n, alpha, _ptr(A), lda, ctypes.byref(S.dist.c()),
                   ctypes.byref(S.seed_state.c()), nnz, _ptr(S.rows), _ptr(S.cols), _ptr(S.vals), ro_s, co_s, beta,
-                  _ptr(B), ldb, st))
+                  _ptr(B), ldb, _opt(_sparse_opts(S, options)), st))
     else:
         raise TypeError("S must be a DenseSkOp or SparseSkOp")
+
+
+def _plan(c: PlanC) -> Plan:
+    return Plan(PLAN_KERNELS.get(c.kernel, str(c.kernel)), int(c.splitk), int(c.tiles), int(c.workgroups))
+
+
+def plan_left(layout, opS, opA, d, n, m, S: DenseSkOp, A, lda, ldb, ro_s=0, co_s=0, dtype="f64",
+              options: Optional[Options] = None) -> Plan:
+    """The kernel, split-K factor and tiles sketch_general_left would use (rbh_lskge3_plan); A is only
+    inspected for its alignment (a device tensor, a host array, or an integer address)."""
+    out = PlanC()
+    a = A if isinstance(A, int) else _ptr(A)
+    _check(getattr(lib, f"rbh_lskge3_plan_{dtype}")(_b(layout), _b(opS), _b(opA), d, n, m, ctypes.byref(S.dist.c()),
+                                                     _ptr(S.buff), _b(S.buff_layout), ro_s, co_s, a, lda, ldb,
+                                                     _opt(options), ctypes.byref(out)))
+    return _plan(out)
+
+
+def plan_right(layout, opA, opS, m, d, n, A, lda, S: DenseSkOp, ldb, ro_s=0, co_s=0, dtype="f64",
+               options: Optional[Options] = None) -> Plan:
+    """The plan of sketch_general_right (rbh_rskge3_plan)."""
+    out = PlanC()
+    a = A if isinstance(A, int) else _ptr(A)
+    _check(getattr(lib, f"rbh_rskge3_plan_{dtype}")(_b(layout), _b(opA), _b(opS), m, d, n, a, lda,
+                                                     ctypes.byref(S.dist.c()), _ptr(S.buff), _b(S.buff_layout), ro_s,
+                                                     co_s, ldb, _opt(options), ctypes.byref(out)))
+    return _plan(out)
 
 
 def require_symmetric(layout, A, n, lda, tol, stream=None) -> None:
@@ -346,7 +470,7 @@ def require_symmetric(layout, A, n, lda, tol, stream=None) -> None:
     _check(fn(_b(layout), _ptr(A), n, lda, tol, _stream(A, stream)))
 
 
-def _sksy(side, layout, d, n, alpha, S, A, lda, beta, B, ldb, ro_s, co_s, tol, stream):
+def _sksy(side, layout, d, n, alpha, S, A, lda, beta, B, ldb, ro_s, co_s, tol, stream, options=None):
     if not isinstance(S, DenseSkOp):
         # a SparseSkOp: require_symmetric + the sparse sketch_general (sksy.hh's SKOP is any operator)
         require_symmetric(layout, A, n, lda, tol, stream)
@@ -354,33 +478,38 @@ def _sksy(side, layout, d, n, alpha, S, A, lda, beta, B, ldb, ro_s, co_s, tol, s
             return sketch_general_left(layout, "N", "N", d, n, n, alpha, S, A, lda, beta, B, ldb, ro_s, co_s, stream)
         return sketch_general_right(layout, "N", "N", n, d, n, alpha, A, lda, S, beta, B, ldb, ro_s, co_s, stream)
     t = _dtype_tag(B)
-    _check(getattr(lib, f"rbh_sketch_symmetric_{t}")(_b(layout), _b(side), d, n, alpha, ctypes.byref(S.dist.c()),
-                                                     ctypes.byref(S.seed_state.c()), _ptr(S.buff), _b(S.buff_layout),
-                                                     ro_s, co_s, _ptr(A), lda, beta, _ptr(B), ldb, tol,
-                                                     _stream(B, stream)))
+    _check(getattr(lib, f"rbh_sketch_symmetric_ex_{t}")(_b(layout), _b(side), d, n, alpha, ctypes.byref(S.dist.c()),
+                                                        ctypes.byref(S.seed_state.c()), _ptr(S.buff),
+                                                        _b(S.buff_layout), ro_s, co_s, _ptr(A), lda, beta, _ptr(B),
+                                                        ldb, tol, _opt(options), _stream(B, stream)))
+
+
+def sketch_symmetric_last_path() -> str:
+    """Which storage this thread's last dense sketch_symmetric read: 'full' or 'upper'."""
+    return "upper" if lib.rbh_sketch_symmetric_last_path() == 1 else "full"
 
 
 def sketch_symmetric_left(layout, d, n, alpha, S, A, lda, beta, B, ldb, ro_s=0, co_s=0, sym_check_tol=0.0,
-                          stream=None):
+                          stream=None, options: Optional[Options] = None):
     """B = alpha S A + beta B, A symmetric n x n in general storage (sksy.hh:300-319 / 520-537)."""
-    _sksy("L", layout, d, n, alpha, S, A, lda, beta, B, ldb, ro_s, co_s, sym_check_tol, stream)
+    _sksy("L", layout, d, n, alpha, S, A, lda, beta, B, ldb, ro_s, co_s, sym_check_tol, stream, options)
 
 
 def sketch_symmetric_right(layout, n, d, alpha, A, lda, S, beta, B, ldb, ro_s=0, co_s=0, sym_check_tol=0.0,
-                           stream=None):
+                           stream=None, options: Optional[Options] = None):
     """B = alpha A S + beta B, A symmetric n x n in general storage (sksy.hh:165-184 / 413-430)."""
-    _sksy("R", layout, d, n, alpha, S, A, lda, beta, B, ldb, ro_s, co_s, sym_check_tol, stream)
+    _sksy("R", layout, d, n, alpha, S, A, lda, beta, B, ldb, ro_s, co_s, sym_check_tol, stream, options)
 
 
 def sketch_symmetric_tri(layout, side, uplo, A_fmt, d, n, alpha, S, A, lda, beta, B, ldb, ro_s=0, co_s=0,
-                         stream=None):
+                         stream=None, options: Optional[Options] = None):
     """Extension: the symmetric sketch reading only triangle `uplo` of A ('F' full storage, 'P' packed);
     side 'L': B = alpha submat(S) A + beta B (d x n), 'R': B = alpha A submat(S) + beta B (n x d)."""
     t = _dtype_tag(B)
-    _check(getattr(lib, f"rbh_sksy_tri_{t}")(_b(layout), _b(side), _b(uplo), _b(A_fmt), d, n, alpha,
-                                             ctypes.byref(S.dist.c()), ctypes.byref(S.seed_state.c()), _ptr(S.buff),
-                                             _b(S.buff_layout), ro_s, co_s, _ptr(A), lda, beta, _ptr(B), ldb,
-                                             _stream(B, stream)))
+    _check(getattr(lib, f"rbh_sksy_tri_ex_{t}")(_b(layout), _b(side), _b(uplo), _b(A_fmt), d, n, alpha,
+                                                ctypes.byref(S.dist.c()), ctypes.byref(S.seed_state.c()),
+                                                _ptr(S.buff), _b(S.buff_layout), ro_s, co_s, _ptr(A), lda, beta,
+                                                _ptr(B), ldb, _opt(options), _stream(B, stream)))
 
 
 def sketch_general(layout, op1, op2, d_or_m, n_or_d, m_or_n, alpha, X, Y, lda_or_none, *args, **kw):
@@ -528,12 +657,15 @@ def abi_version() -> int:
     return int(lib.rbh_abi_version())
 
 
-def release_workspaces(stream=None) -> None:
+def release_workspaces(stream=None, all_streams: Optional[bool] = None) -> None:
     """Synchronise and free the library's idle workspace blocks: those of `stream` (a torch stream
-    or a raw hipStream_t), or of every stream of the current device when None (rbh_release_workspaces)."""
+    or a raw hipStream_t), or of every stream of the current device with all_streams (the default
+    when no stream is given) (rbh_release_workspaces)."""
     if stream is not None and hasattr(stream, "cuda_stream"):
         stream = stream.cuda_stream
-    _check(lib.rbh_release_workspaces(c_vp(stream) if stream else None))
+    if all_streams is None:
+        all_streams = stream is None
+    _check(lib.rbh_release_workspaces(c_vp(stream) if stream else None, 1 if all_streams else 0))
 
 
 def unpack_shards(src, nshards, rows, run, dst, row_stride, shard_stride, stream=None) -> None:
@@ -542,6 +674,10 @@ def unpack_shards(src, nshards, rows, run, dst, row_stride, shard_stride, stream
     dst[g * shard_stride + j * row_stride + i]. src and dst: 1-D device tensors of one dtype."""
     if src.dtype != dst.dtype:
         raise TypeError("unpack_shards: src and dst dtypes differ")
+    if not (src.is_cuda and dst.is_cuda) or src.device != dst.device:
+        raise ValueError("unpack_shards: src and dst must be tensors on one GPU")
+    if not (src.is_contiguous() and dst.is_contiguous()):
+        raise ValueError("unpack_shards: src and dst must be contiguous")
     if nshards * rows * run > src.numel() or (nshards and rows and run and
                                               (nshards - 1) * shard_stride + (rows - 1) * row_stride + run > dst.numel()):
         raise ValueError("unpack_shards: shapes exceed the buffers")
@@ -555,5 +691,6 @@ __all__ = [
     "sketch_symmetric_right", "require_symmetric", "dense_next_state", "sparse_next_state", "abi_version", "lib",
     "LIB_PATH", "kernel_timing", "kernel_times_ms", "sketch_vector", "sketch_vector_full", "COOMatrix",
     "CSRMatrix", "CSCMatrix", "sketch_sparse", "sketch_sparse_left", "sketch_sparse_right", "spmm",
-    "sketch_symmetric_tri", "release_workspaces", "unpack_shards",
+    "sketch_symmetric_tri", "release_workspaces", "unpack_shards", "Options", "Plan", "plan_left", "plan_right",
+    "sketch_symmetric_last_path", "fill_sparse_op", "sparse_last_path",
 ]

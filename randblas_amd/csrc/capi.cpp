@@ -120,7 +120,11 @@ hipError_t ws_alloc(void **p, size_t bytes, hipStream_t s) {
         const size_t last = a.blocks.empty() ? 0 : a.blocks.back().cap;
         size_t cap = 2 * last > WS_MIN_BLOCK ? 2 * last : WS_MIN_BLOCK;
         if (cap < need) cap = need;
-        if (retained_bytes(dev) + cap > WS_RETAIN_CAP) {   // over the cap: release every idle block
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &cs) != hipSuccess) { (void)hipGetLastError(); cs = hipStreamCaptureStatusNone; }
+        // over the cap: release every idle block (not while the stream is being captured into a
+        // graph, where a device synchronisation would invalidate the capture)
+        if (cs == hipStreamCaptureStatusNone && retained_bytes(dev) + cap > WS_RETAIN_CAP) {
             (void)hipDeviceSynchronize();
             for (auto &kv : g_arenas)
                 if (kv.first.first == dev && &kv.second != &a) arena_release_idle(kv.second);
@@ -188,6 +192,7 @@ hipError_t ws_release(hipStream_t s, bool all) {
 namespace {
 
 thread_local std::string g_last_error;
+thread_local int g_sksy_path = 0;   // rbh_sketch_symmetric_path: storage the last sketch_symmetric read
 
 int set_error(int code, const char *fmt, ...) {
     char buf[1024];
@@ -373,6 +378,20 @@ template <> hipError_t launch_scale_t<float>(int64_t M, int64_t N, float b, floa
     return launch_scale_f32(M, N, b, C, ldc, s);
 }
 
+// rbh_options (NULL: the defaults): checked, then copied into the canonical problem
+int check_options(const rbh_options *opt) {
+    if (!opt) return RBH_OK;
+    RBH_REQUIRE(opt->splitk >= 0);
+    RBH_REQUIRE(opt->materialise == 0 || opt->materialise == 1);
+    RBH_REQUIRE(opt->sksy_triangle == 0 || opt->sksy_triangle == 1);
+    RBH_REQUIRE(opt->sparse_filled == 0 || opt->sparse_filled == 1);
+    return RBH_OK;
+}
+void apply_options(GemmProblem &p, const rbh_options *opt) {
+    p.split_req = opt ? opt->splitk : 0;
+    p.materialise = opt ? opt->materialise : 0;
+}
+
 // Canonical dense GEMM launch: X/Y either generated (S window) or memory.
 template <typename T>
 int run_dense(GemmProblem &p, hipStream_t s) {
@@ -400,7 +419,9 @@ void build_right(GemmProblem &p, char layout, char opA, char opS, int64_t m, int
 template <typename T>
 int lskge3(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, T alpha, const rbh_dense_dist *D,
            const rbh_state *seed, const T *S_buff, char S_layout, int64_t ro_s, int64_t co_s, const T *A,
-           int64_t lda, T beta, T *B, int64_t ldb, void *stream) {
+           int64_t lda, T beta, T *B, int64_t ldb, const rbh_options *opt, void *stream) {
+    int rc = check_options(opt);
+    if (rc) return rc;
     RBH_REQUIRE(layout == 'C' || layout == 'R');
     RBH_REQUIRE(opS == 'N' || opS == 'T');
     RBH_REQUIRE(opA == 'N' || opA == 'T');
@@ -432,7 +453,8 @@ int lskge3(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, T a
     RBH_HIP(st.map(S_buff, sizeof(T) * D->n_rows * D->n_cols, true, false, &dS));
     GemmProblem p{};
     build_left<T>(p, layout, opS, opA, d, n, m, alpha, beta, D, seed, dS, S_layout, ro_s, co_s, dA, lda, dB, ldb);
-    int rc = run_dense<T>(p, s);
+    apply_options(p, opt);
+    rc = run_dense<T>(p, s);
     if (rc) return rc;
     RBH_HIP(st.finish());
     return RBH_OK;
@@ -486,7 +508,9 @@ void build_left(GemmProblem &p, char layout, char opS, char opA, int64_t d, int6
 template <typename T>
 int rskge3(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, T alpha, const T *A, int64_t lda,
            const rbh_dense_dist *D, const rbh_state *seed, const T *S_buff, char S_layout, int64_t ro_s,
-           int64_t co_s, T beta, T *B, int64_t ldb, void *stream) {
+           int64_t co_s, T beta, T *B, int64_t ldb, const rbh_options *opt, void *stream) {
+    int rc = check_options(opt);
+    if (rc) return rc;
     RBH_REQUIRE(layout == 'C' || layout == 'R');
     RBH_REQUIRE(opS == 'N' || opS == 'T');
     RBH_REQUIRE(opA == 'N' || opA == 'T');
@@ -518,7 +542,8 @@ int rskge3(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, T a
     RBH_HIP(st.map(S_buff, sizeof(T) * D->n_rows * D->n_cols, true, false, &dS));
     GemmProblem p{};
     build_right<T>(p, layout, opA, opS, m, d, n, alpha, beta, dA, lda, D, seed, dS, S_layout, ro_s, co_s, dB, ldb);
-    int rc = run_dense<T>(p, s);
+    apply_options(p, opt);
+    rc = run_dense<T>(p, s);
     if (rc) return rc;
     RBH_HIP(st.finish());
     return RBH_OK;
@@ -724,7 +749,10 @@ int check_left_spmm(char layout, char opS, char opB, int64_t d, int64_t n, int64
 template <typename T>
 int sparse_common(SparseApply &p, const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz, const int64_t *rows,
                   const int64_t *cols, const T *vals, const T *A, int64_t A_extent, T *B, char layout,
-                  int64_t B_rows, int64_t B_cols, int64_t ldb, T beta, hipStream_t s) {
+                  int64_t B_rows, int64_t B_cols, int64_t ldb, T beta, const rbh_options *opt, hipStream_t s) {
+    int rc = check_options(opt);
+    if (rc) return rc;
+    p.arrays_filled = opt ? opt->sparse_filled : 0;
     Stager st(s);
     void *dA, *dB;
     RBH_HIP(st.map(A, sizeof(T) * A_extent, true, false, &dA));
@@ -751,7 +779,7 @@ int sparse_common(SparseApply &p, const rbh_sparse_dist *D, const rbh_state *see
 template <typename T>
 int lskges(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, T alpha, const rbh_sparse_dist *D,
            const rbh_state *seed, int64_t nnz, const int64_t *rows, const int64_t *cols, const T *vals, int64_t ro_s,
-           int64_t co_s, const T *A, int64_t lda, T beta, T *B, int64_t ldb, void *stream) {
+           int64_t co_s, const T *A, int64_t lda, T beta, T *B, int64_t ldb, const rbh_options *opt, void *stream) {
     RBH_REQUIRE(layout == 'C' || layout == 'R');
     RBH_REQUIRE(opS == 'N' || opS == 'T');
     RBH_REQUIRE(opA == 'N' || opA == 'T');
@@ -774,7 +802,7 @@ int lskges(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, T a
     else { p.ysk = opA == 'N' ? lda : 1; p.ysj = opA == 'N' ? 1 : lda; }
     const int64_t rows_A = opA == 'N' ? m : n, cols_A = opA == 'N' ? n : m;
     return sparse_common<T>(p, D, seed, nnz, rows, cols, vals, A, extent(layout, rows_A, cols_A, lda), B, layout,
-                            d, n, ldb, beta, (hipStream_t)stream);
+                            d, n, ldb, beta, opt, (hipStream_t)stream);
 }
 
 // right: B = alpha op(A) op(submat(S)) + beta B   (sparse::rskges, skge.hh:616-641 -> right_spmm,
@@ -782,7 +810,8 @@ int lskges(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, T a
 template <typename T>
 int rskges(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, T alpha, const T *A, int64_t lda,
            const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz, const int64_t *rows, const int64_t *cols,
-           const T *vals, int64_t ro_s, int64_t co_s, T beta, T *B, int64_t ldb, void *stream) {
+           const T *vals, int64_t ro_s, int64_t co_s, T beta, T *B, int64_t ldb, const rbh_options *opt,
+           void *stream) {
     RBH_REQUIRE(layout == 'C' || layout == 'R');
     RBH_REQUIRE(opS == 'N' || opS == 'T');
     RBH_REQUIRE(opA == 'N' || opA == 'T');
@@ -809,7 +838,7 @@ int rskges(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, T a
     else { p.ysk = opA == 'N' ? 1 : lda; p.ysj = opA == 'N' ? lda : 1; }
     const int64_t rows_A = opA == 'N' ? m : n, cols_A = opA == 'N' ? n : m;
     return sparse_common<T>(p, D, seed, nnz, rows, cols, vals, A, extent(layout, rows_A, cols_A, lda), B, layout,
-                            m, d, ldb, beta, (hipStream_t)stream);
+                            m, d, ldb, beta, opt, (hipStream_t)stream);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1105,7 +1134,7 @@ template <> hipError_t launch_symz_t<float>(int t, const float *A, int64_t lda, 
 template <typename T>
 int sksy_tri_dev(char layout, char side, char uplo, char fmt, int64_t d, int64_t n, T alpha, const rbh_dense_dist *D,
                  const rbh_state *seed, const void *dS, char S_layout, int64_t ro_s, int64_t co_s, const void *dA,
-                 int64_t lda, T beta, void *dB, int64_t ldb, hipStream_t s) {
+                 int64_t lda, T beta, void *dB, int64_t ldb, const rbh_options *opt, hipStream_t s) {
     GemmProblem p{};
     const int64_t lda_eff = fmt == 'F' ? lda : n;
     if (side == 'L') build_left<T>(p, layout, 'N', 'N', d, n, n, alpha, beta, D, seed, dS, S_layout, ro_s, co_s, dA,
@@ -1113,6 +1142,7 @@ int sksy_tri_dev(char layout, char side, char uplo, char fmt, int64_t d, int64_t
     else build_right<T>(p, layout, 'N', 'N', n, d, n, alpha, beta, dA, lda_eff, D, seed, dS, S_layout, ro_s, co_s, dB,
                         ldb);
     if (p.M <= 0 || p.N <= 0) return RBH_OK;
+    apply_options(p, opt);
     // A as the operand (o, k) -> storage o*lda + k, valid for every layout by symmetry
     const bool a_is_x = side == 'L' ? layout == 'R' : layout == 'C';
     MemOperand &mo = a_is_x ? p.xm : p.ym;
@@ -1169,8 +1199,10 @@ int check_sksy(char layout, char side, int64_t d, int64_t n, const rbh_dense_dis
 template <typename T>
 int sksy_tri(char layout, char side, char uplo, char fmt, int64_t d, int64_t n, T alpha, const rbh_dense_dist *D,
              const rbh_state *seed, const T *S_buff, char S_layout, int64_t ro_s, int64_t co_s, const T *A, int64_t lda,
-             T beta, T *B, int64_t ldb, void *stream) {
-    int rc = check_sksy(layout, side, d, n, D, seed, S_buff, S_layout, ro_s, co_s, ldb);
+             T beta, T *B, int64_t ldb, const rbh_options *opt, void *stream) {
+    int rc = check_options(opt);
+    if (rc) return rc;
+    rc = check_sksy(layout, side, d, n, D, seed, S_buff, S_layout, ro_s, co_s, ldb);
     if (rc) return rc;
     RBH_REQUIRE(uplo == 'U' || uplo == 'L');
     RBH_REQUIRE(fmt == 'F' || fmt == 'P');
@@ -1183,23 +1215,26 @@ int sksy_tri(char layout, char side, char uplo, char fmt, int64_t d, int64_t n, 
     RBH_HIP(st.map_out(B, sizeof(T), layout, side == 'L' ? d : n, side == 'L' ? n : d, ldb, beta != (T)0, &dB));
     RBH_HIP(st.map(S_buff, sizeof(T) * D->n_rows * D->n_cols, true, false, &dS));
     rc = sksy_tri_dev<T>(layout, side, uplo, fmt, d, n, alpha, D, seed, dS, S_layout, ro_s, co_s, dA, lda, beta, dB,
-                         ldb, s);
+                         ldb, opt, s);
     if (rc) return rc;
     RBH_HIP(st.finish());
     return RBH_OK;
 }
 
 // sketch_symmetric (sksy.hh:165-537) in one call: util::require_symmetric with tol (skipped when
-// tol < 0, util.hh:166-168), then sketch_general on full storage. With RBH_SKSY_TRI=1, and when the
-// check ran and found A bitwise symmetric, only the upper triangle is read instead: the operand
-// tiles are then identical, so the result is the full-storage product's bit for bit. It is not the
-// default: every stored tile is then fetched twice (once per role), so the fabric traffic is the
-// same, and the mirror / diagonal tiles cost 4.5 % at C5.
+// tol < 0, util.hh:166-168), then sketch_general on full storage. With opt->sksy_triangle = 1, and
+// when the check ran and found A bitwise symmetric, only the upper triangle is read instead: the
+// operand tiles are then identical, so the result is the full-storage product's bit for bit. It is
+// not the default: every stored tile is then fetched twice (once per role), so the fabric traffic
+// is the same, and the mirror / diagonal tiles cost 4.5 % at C5.
+// rbh_sketch_symmetric_last_path() reports which storage the calling thread's last call read.
 template <typename T>
 int sketch_symmetric(char layout, char side, int64_t d, int64_t n, T alpha, const rbh_dense_dist *D,
                      const rbh_state *seed, const T *S_buff, char S_layout, int64_t ro_s, int64_t co_s, const T *A,
-                     int64_t lda, T beta, T *B, int64_t ldb, T tol, void *stream) {
-    int rc = check_sksy(layout, side, d, n, D, seed, S_buff, S_layout, ro_s, co_s, ldb);
+                     int64_t lda, T beta, T *B, int64_t ldb, T tol, const rbh_options *opt, void *stream) {
+    int rc = check_options(opt);
+    if (rc) return rc;
+    rc = check_sksy(layout, side, d, n, D, seed, S_buff, S_layout, ro_s, co_s, ldb);
     if (rc) return rc;
     RBH_REQUIRE(lda >= n);
     hipStream_t s = (hipStream_t)stream;
@@ -1214,20 +1249,52 @@ int sketch_symmetric(char layout, char side, int64_t d, int64_t n, T alpha, cons
     }
     RBH_HIP(st.map_out(B, sizeof(T), layout, side == 'L' ? d : n, side == 'L' ? n : d, ldb, beta != (T)0, &dB));
     RBH_HIP(st.map(S_buff, sizeof(T) * D->n_rows * D->n_cols, true, false, &dS));
-    static const bool use_tri = [] { const char *e = getenv("RBH_SKSY_TRI"); return e && e[0] == '1'; }();
+    const bool use_tri = opt && opt->sksy_triangle;
+    g_sksy_path = 0;
     if (!(flags & 2) && use_tri) {
+        g_sksy_path = 1;
         rc = sksy_tri_dev<T>(layout, side, 'U', 'F', d, n, alpha, D, seed, dS, S_layout, ro_s, co_s, dA, lda, beta,
-                             dB, ldb, s);
+                             dB, ldb, opt, s);
     } else {
         GemmProblem p{};
         if (side == 'L') build_left<T>(p, layout, 'N', 'N', d, n, n, alpha, beta, D, seed, dS, S_layout, ro_s, co_s,
                                        dA, lda, dB, ldb);
         else build_right<T>(p, layout, 'N', 'N', n, d, n, alpha, beta, dA, lda, D, seed, dS, S_layout, ro_s, co_s, dB,
                             ldb);
+        apply_options(p, opt);
         rc = run_dense<T>(p, s);
     }
     if (rc) return rc;
     RBH_HIP(st.finish());
+    return RBH_OK;
+}
+
+// rbh_lskge3_plan / rbh_rskge3_plan: the kernel, tiles and split-K factor the sketch call with these
+// arguments would launch (left: (M1, M2, M3) = (d, n, m); right: (m, d, n)). Pointers are only
+// inspected (alignment), never dereferenced; the operator is the fused one unless S_buff is given.
+template <typename T>
+int dense_plan(bool left, char layout, char opS, char opA, int64_t M1, int64_t M2, int64_t M3, const rbh_dense_dist *D,
+               const T *S_buff, char S_layout, int64_t ro_s, int64_t co_s, const T *A, int64_t lda, int64_t ldb,
+               const rbh_options *opt, rbh_plan *plan) {
+    int rc = check_options(opt);
+    if (rc) return rc;
+    RBH_REQUIRE(plan != nullptr && D != nullptr);
+    RBH_REQUIRE(layout == 'C' || layout == 'R');
+    RBH_REQUIRE(opS == 'N' || opS == 'T');
+    RBH_REQUIRE(opA == 'N' || opA == 'T');
+    RBH_REQUIRE(M1 >= 0 && M2 >= 0 && M3 >= 0 && ro_s >= 0 && co_s >= 0);
+    static const rbh_state zero{};
+    GemmProblem p{};
+    if (left) build_left<T>(p, layout, opS, opA, M1, M2, M3, (T)1, (T)0, D, &zero, S_buff, S_layout, ro_s, co_s, A, lda,
+                            nullptr, ldb);
+    else build_right<T>(p, layout, opA, opS, M1, M2, M3, (T)1, (T)0, A, lda, D, &zero, S_buff, S_layout, ro_s, co_s,
+                        nullptr, ldb);
+    apply_options(p, opt);
+    const GemmPlan g = sizeof(T) == 8 ? plan_gemm_f64(p) : plan_gemm_f32(p);
+    plan->kernel = g.kernel;
+    plan->splitk = g.splitk;
+    plan->tiles = g.tiles;
+    plan->workgroups = g.workgroups;
     return RBH_OK;
 }
 
@@ -1238,10 +1305,10 @@ int sketch_symmetric(char layout, char side, int64_t d, int64_t n, T alpha, cons
 // =============================================================================================
 extern "C" {
 
-int rbh_abi_version(void) { return 1; }
+int rbh_abi_version(void) { return 2; }
 
-int rbh_release_workspaces(void *stream) {
-    const hipError_t e = ws_release((hipStream_t)stream, stream == nullptr);
+int rbh_release_workspaces(void *stream, int all_streams) {
+    const hipError_t e = ws_release((hipStream_t)stream, all_streams != 0);
     if (e != hipSuccess) return set_error(RBH_ERR_HIP, "HIP error %s in rbh_release_workspaces", hipGetErrorName(e));
     return RBH_OK;
 }
@@ -1254,6 +1321,7 @@ int rbh_unpack_shards(const void *src, int64_t nshards, int64_t rows, int64_t ru
     RBH_REQUIRE(shard_stride >= 0);
     if (nshards == 0 || rows == 0 || run == 0) return RBH_OK;
     RBH_REQUIRE(src != nullptr && dst != nullptr);
+    RBH_REQUIRE(rbh_is_device_pointer(src) && rbh_is_device_pointer(dst));
     RBH_HIP(launch_unpack_shards(src, nshards, rows, run, dst, row_stride, shard_stride, elem_bytes, (hipStream_t)stream));
     return RBH_OK;
 }
@@ -1317,25 +1385,25 @@ int rbh_lskge3_f64(char layout, char opS, char opA, int64_t d, int64_t n, int64_
                    const rbh_dense_dist *D, const rbh_state *seed, const double *S_buff, char S_layout, int64_t ro_s,
                    int64_t co_s, const double *A, int64_t lda, double beta, double *B, int64_t ldb, void *stream) {
     return lskge3<double>(layout, opS, opA, d, n, m, alpha, D, seed, S_buff, S_layout, ro_s, co_s, A, lda, beta, B,
-                          ldb, stream);
+                          ldb, nullptr, stream);
 }
 int rbh_lskge3_f32(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, float alpha,
                    const rbh_dense_dist *D, const rbh_state *seed, const float *S_buff, char S_layout, int64_t ro_s,
                    int64_t co_s, const float *A, int64_t lda, float beta, float *B, int64_t ldb, void *stream) {
     return lskge3<float>(layout, opS, opA, d, n, m, alpha, D, seed, S_buff, S_layout, ro_s, co_s, A, lda, beta, B,
-                         ldb, stream);
+                         ldb, nullptr, stream);
 }
 int rbh_rskge3_f64(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, double alpha, const double *A,
                    int64_t lda, const rbh_dense_dist *D, const rbh_state *seed, const double *S_buff, char S_layout,
                    int64_t ro_s, int64_t co_s, double beta, double *B, int64_t ldb, void *stream) {
     return rskge3<double>(layout, opA, opS, m, d, n, alpha, A, lda, D, seed, S_buff, S_layout, ro_s, co_s, beta, B,
-                          ldb, stream);
+                          ldb, nullptr, stream);
 }
 int rbh_rskge3_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, float alpha, const float *A,
                    int64_t lda, const rbh_dense_dist *D, const rbh_state *seed, const float *S_buff, char S_layout,
                    int64_t ro_s, int64_t co_s, float beta, float *B, int64_t ldb, void *stream) {
     return rskge3<float>(layout, opA, opS, m, d, n, alpha, A, lda, D, seed, S_buff, S_layout, ro_s, co_s, beta, B,
-                         ldb, stream);
+                         ldb, nullptr, stream);
 }
 
 int rbh_lsksp3_f64(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, double alpha,
@@ -1376,28 +1444,28 @@ int rbh_lskges_f64(char layout, char opS, char opA, int64_t d, int64_t n, int64_
                    const int64_t *cols, const double *vals, int64_t ro_s, int64_t co_s, const double *A, int64_t lda,
                    double beta, double *B, int64_t ldb, void *stream) {
     return lskges<double>(layout, opS, opA, d, n, m, alpha, D, seed, nnz, rows, cols, vals, ro_s, co_s, A, lda, beta,
-                          B, ldb, stream);
+                         B, ldb, nullptr, stream);
 }
 int rbh_lskges_f32(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, float alpha,
                    const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz, const int64_t *rows,
                    const int64_t *cols, const float *vals, int64_t ro_s, int64_t co_s, const float *A, int64_t lda,
                    float beta, float *B, int64_t ldb, void *stream) {
     return lskges<float>(layout, opS, opA, d, n, m, alpha, D, seed, nnz, rows, cols, vals, ro_s, co_s, A, lda, beta,
-                         B, ldb, stream);
+                         B, ldb, nullptr, stream);
 }
 int rbh_rskges_f64(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, double alpha, const double *A,
                    int64_t lda, const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz, const int64_t *rows,
                    const int64_t *cols, const double *vals, int64_t ro_s, int64_t co_s, double beta, double *B,
                    int64_t ldb, void *stream) {
     return rskges<double>(layout, opA, opS, m, d, n, alpha, A, lda, D, seed, nnz, rows, cols, vals, ro_s, co_s, beta,
-                          B, ldb, stream);
+                         B, ldb, nullptr, stream);
 }
 int rbh_rskges_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, float alpha, const float *A,
                    int64_t lda, const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz, const int64_t *rows,
                    const int64_t *cols, const float *vals, int64_t ro_s, int64_t co_s, float beta, float *B,
                    int64_t ldb, void *stream) {
     return rskges<float>(layout, opA, opS, m, d, n, alpha, A, lda, D, seed, nnz, rows, cols, vals, ro_s, co_s, beta,
-                         B, ldb, stream);
+                         B, ldb, nullptr, stream);
 }
 
 int rbh_spmm_left_f64(char layout, char opA, char opB, int64_t m, int64_t n, int64_t k, double alpha, char A_fmt,
@@ -1440,26 +1508,26 @@ int rbh_sketch_symmetric_f64(char layout, char side, int64_t d, int64_t n, doubl
                              const double *A, int64_t lda, double beta, double *B, int64_t ldb, double sym_check_tol,
                              void *stream) {
     return sketch_symmetric<double>(layout, side, d, n, alpha, D, seed, S_buff, S_layout, ro_s, co_s, A, lda, beta, B,
-                                    ldb, sym_check_tol, stream);
+                                    ldb, sym_check_tol, nullptr, stream);
 }
 int rbh_sketch_symmetric_f32(char layout, char side, int64_t d, int64_t n, float alpha, const rbh_dense_dist *D,
                              const rbh_state *seed, const float *S_buff, char S_layout, int64_t ro_s, int64_t co_s,
                              const float *A, int64_t lda, float beta, float *B, int64_t ldb, float sym_check_tol,
                              void *stream) {
     return sketch_symmetric<float>(layout, side, d, n, alpha, D, seed, S_buff, S_layout, ro_s, co_s, A, lda, beta, B,
-                                   ldb, sym_check_tol, stream);
+                                   ldb, sym_check_tol, nullptr, stream);
 }
 int rbh_sksy_tri_f64(char layout, char side, char uplo, char A_fmt, int64_t d, int64_t n, double alpha,
                      const rbh_dense_dist *D, const rbh_state *seed, const double *S_buff, char S_layout, int64_t ro_s,
                      int64_t co_s, const double *A, int64_t lda, double beta, double *B, int64_t ldb, void *stream) {
     return sksy_tri<double>(layout, side, uplo, A_fmt, d, n, alpha, D, seed, S_buff, S_layout, ro_s, co_s, A, lda, beta,
-                            B, ldb, stream);
+                            B, ldb, nullptr, stream);
 }
 int rbh_sksy_tri_f32(char layout, char side, char uplo, char A_fmt, int64_t d, int64_t n, float alpha,
                      const rbh_dense_dist *D, const rbh_state *seed, const float *S_buff, char S_layout, int64_t ro_s,
                      int64_t co_s, const float *A, int64_t lda, float beta, float *B, int64_t ldb, void *stream) {
     return sksy_tri<float>(layout, side, uplo, A_fmt, d, n, alpha, D, seed, S_buff, S_layout, ro_s, co_s, A, lda, beta,
-                           B, ldb, stream);
+                           B, ldb, nullptr, stream);
 }
 
 int rbh_require_symmetric_f64(char layout, const double *A, int64_t n, int64_t lda, double tol, void *stream) {
@@ -1467,6 +1535,116 @@ int rbh_require_symmetric_f64(char layout, const double *A, int64_t n, int64_t l
 }
 int rbh_require_symmetric_f32(char layout, const float *A, int64_t n, int64_t lda, float tol, void *stream) {
     return require_symmetric<float>(layout, A, n, lda, tol, stream);
+}
+
+// ---- per-call options and plans ------------------------------------------------------------
+int rbh_lskge3_ex_f64(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, double alpha,
+                      const rbh_dense_dist *D, const rbh_state *seed, const double *S_buff, char S_layout,
+                      int64_t ro_s, int64_t co_s, const double *A, int64_t lda, double beta, double *B, int64_t ldb,
+                      const rbh_options *opt, void *stream) {
+    return lskge3<double>(layout, opS, opA, d, n, m, alpha, D, seed, S_buff, S_layout, ro_s, co_s, A, lda, beta, B,
+                          ldb, opt, stream);
+}
+int rbh_lskge3_ex_f32(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, float alpha,
+                      const rbh_dense_dist *D, const rbh_state *seed, const float *S_buff, char S_layout,
+                      int64_t ro_s, int64_t co_s, const float *A, int64_t lda, float beta, float *B, int64_t ldb,
+                      const rbh_options *opt, void *stream) {
+    return lskge3<float>(layout, opS, opA, d, n, m, alpha, D, seed, S_buff, S_layout, ro_s, co_s, A, lda, beta, B,
+                         ldb, opt, stream);
+}
+int rbh_rskge3_ex_f64(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, double alpha, const double *A,
+                      int64_t lda, const rbh_dense_dist *D, const rbh_state *seed, const double *S_buff, char S_layout,
+                      int64_t ro_s, int64_t co_s, double beta, double *B, int64_t ldb, const rbh_options *opt,
+                      void *stream) {
+    return rskge3<double>(layout, opA, opS, m, d, n, alpha, A, lda, D, seed, S_buff, S_layout, ro_s, co_s, beta, B,
+                          ldb, opt, stream);
+}
+int rbh_rskge3_ex_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, float alpha, const float *A,
+                      int64_t lda, const rbh_dense_dist *D, const rbh_state *seed, const float *S_buff, char S_layout,
+                      int64_t ro_s, int64_t co_s, float beta, float *B, int64_t ldb, const rbh_options *opt,
+                      void *stream) {
+    return rskge3<float>(layout, opA, opS, m, d, n, alpha, A, lda, D, seed, S_buff, S_layout, ro_s, co_s, beta, B,
+                         ldb, opt, stream);
+}
+int rbh_sketch_symmetric_ex_f64(char layout, char side, int64_t d, int64_t n, double alpha, const rbh_dense_dist *D,
+                                const rbh_state *seed, const double *S_buff, char S_layout, int64_t ro_s,
+                                int64_t co_s, const double *A, int64_t lda, double beta, double *B, int64_t ldb,
+                                double sym_check_tol, const rbh_options *opt, void *stream) {
+    return sketch_symmetric<double>(layout, side, d, n, alpha, D, seed, S_buff, S_layout, ro_s, co_s, A, lda, beta, B,
+                                    ldb, sym_check_tol, opt, stream);
+}
+int rbh_sketch_symmetric_ex_f32(char layout, char side, int64_t d, int64_t n, float alpha, const rbh_dense_dist *D,
+                                const rbh_state *seed, const float *S_buff, char S_layout, int64_t ro_s,
+                                int64_t co_s, const float *A, int64_t lda, float beta, float *B, int64_t ldb,
+                                float sym_check_tol, const rbh_options *opt, void *stream) {
+    return sketch_symmetric<float>(layout, side, d, n, alpha, D, seed, S_buff, S_layout, ro_s, co_s, A, lda, beta, B,
+                                   ldb, sym_check_tol, opt, stream);
+}
+int rbh_sketch_symmetric_last_path(void) { return g_sksy_path; }
+int rbh_sparse_last_path(void) { return sparse_last_path(); }
+int rbh_sksy_tri_ex_f64(char layout, char side, char uplo, char A_fmt, int64_t d, int64_t n, double alpha,
+                        const rbh_dense_dist *D, const rbh_state *seed, const double *S_buff, char S_layout,
+                        int64_t ro_s, int64_t co_s, const double *A, int64_t lda, double beta, double *B, int64_t ldb,
+                        const rbh_options *opt, void *stream) {
+    return sksy_tri<double>(layout, side, uplo, A_fmt, d, n, alpha, D, seed, S_buff, S_layout, ro_s, co_s, A, lda, beta,
+                            B, ldb, opt, stream);
+}
+int rbh_sksy_tri_ex_f32(char layout, char side, char uplo, char A_fmt, int64_t d, int64_t n, float alpha,
+                        const rbh_dense_dist *D, const rbh_state *seed, const float *S_buff, char S_layout,
+                        int64_t ro_s, int64_t co_s, const float *A, int64_t lda, float beta, float *B, int64_t ldb,
+                        const rbh_options *opt, void *stream) {
+    return sksy_tri<float>(layout, side, uplo, A_fmt, d, n, alpha, D, seed, S_buff, S_layout, ro_s, co_s, A, lda, beta,
+                           B, ldb, opt, stream);
+}
+
+int rbh_lskges_ex_f64(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, double alpha,
+                      const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz, const int64_t *rows,
+                      const int64_t *cols, const double *vals, int64_t ro_s, int64_t co_s, const double *A, int64_t lda,
+                      double beta, double *B, int64_t ldb, const rbh_options *opt, void *stream) {
+    return lskges<double>(layout, opS, opA, d, n, m, alpha, D, seed, nnz, rows, cols, vals, ro_s, co_s, A, lda, beta,
+                          B, ldb, opt, stream);
+}
+int rbh_lskges_ex_f32(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, float alpha,
+                      const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz, const int64_t *rows,
+                      const int64_t *cols, const float *vals, int64_t ro_s, int64_t co_s, const float *A, int64_t lda,
+                      float beta, float *B, int64_t ldb, const rbh_options *opt, void *stream) {
+    return lskges<float>(layout, opS, opA, d, n, m, alpha, D, seed, nnz, rows, cols, vals, ro_s, co_s, A, lda, beta,
+                         B, ldb, opt, stream);
+}
+int rbh_rskges_ex_f64(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, double alpha, const double *A,
+                      int64_t lda, const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz, const int64_t *rows,
+                      const int64_t *cols, const double *vals, int64_t ro_s, int64_t co_s, double beta, double *B,
+                      int64_t ldb, const rbh_options *opt, void *stream) {
+    return rskges<double>(layout, opA, opS, m, d, n, alpha, A, lda, D, seed, nnz, rows, cols, vals, ro_s, co_s, beta,
+                          B, ldb, opt, stream);
+}
+int rbh_rskges_ex_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, float alpha, const float *A,
+                      int64_t lda, const rbh_sparse_dist *D, const rbh_state *seed, int64_t nnz, const int64_t *rows,
+                      const int64_t *cols, const float *vals, int64_t ro_s, int64_t co_s, float beta, float *B,
+                      int64_t ldb, const rbh_options *opt, void *stream) {
+    return rskges<float>(layout, opA, opS, m, d, n, alpha, A, lda, D, seed, nnz, rows, cols, vals, ro_s, co_s, beta,
+                         B, ldb, opt, stream);
+}
+
+int rbh_lskge3_plan_f64(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, const rbh_dense_dist *D,
+                        const double *S_buff, char S_layout, int64_t ro_s, int64_t co_s, const double *A, int64_t lda,
+                        int64_t ldb, const rbh_options *opt, rbh_plan *plan) {
+    return dense_plan<double>(true, layout, opS, opA, d, n, m, D, S_buff, S_layout, ro_s, co_s, A, lda, ldb, opt, plan);
+}
+int rbh_lskge3_plan_f32(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, const rbh_dense_dist *D,
+                        const float *S_buff, char S_layout, int64_t ro_s, int64_t co_s, const float *A, int64_t lda,
+                        int64_t ldb, const rbh_options *opt, rbh_plan *plan) {
+    return dense_plan<float>(true, layout, opS, opA, d, n, m, D, S_buff, S_layout, ro_s, co_s, A, lda, ldb, opt, plan);
+}
+int rbh_rskge3_plan_f64(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, const double *A, int64_t lda,
+                        const rbh_dense_dist *D, const double *S_buff, char S_layout, int64_t ro_s, int64_t co_s,
+                        int64_t ldb, const rbh_options *opt, rbh_plan *plan) {
+    return dense_plan<double>(false, layout, opS, opA, m, d, n, D, S_buff, S_layout, ro_s, co_s, A, lda, ldb, opt, plan);
+}
+int rbh_rskge3_plan_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, const float *A, int64_t lda,
+                        const rbh_dense_dist *D, const float *S_buff, char S_layout, int64_t ro_s, int64_t co_s,
+                        int64_t ldb, const rbh_options *opt, rbh_plan *plan) {
+    return dense_plan<float>(false, layout, opS, opA, m, d, n, D, S_buff, S_layout, ro_s, co_s, A, lda, ldb, opt, plan);
 }
 
 }  // extern "C"

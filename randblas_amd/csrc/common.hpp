@@ -57,7 +57,31 @@ struct GemmProblem {
     // The generated operand materialised by the launcher (wide kernels, launch_gemm): element (o, k)
     // at gmat[o * K + k]; null = drawn inside the kernel.
     const void *gmat;
+    // Per-call requests (rbh_options of the C ABI): split_req 0 = automatic split-K, 1 = never,
+    // s >= 2 = exactly s slices; materialise 1 = draw the operator window into a workspace first.
+    int split_req;
+    int materialise;
 };
+
+// The kernel launch_gemm_* would run for a problem, and its split-K factor (rbh_plan).
+enum PlanKernel : int {
+    PLAN_NONE = 0,        // empty output
+    PLAN_SCALE = 1,       // K == 0 or alpha == 0: C = beta C only
+    PLAN_GENERIC = 2,     // skge_gemm_kernel (any operand modes, explicit S buffers)
+    PLAN_FUSED = 3,       // skge_fused_kernel
+    PLAN_WIDE = 4,        // skge_wide_kernel (f64)
+    PLAN_WIDE32 = 5,      // skge_wide32_kernel (f32)
+    PLAN_WIDE_TRI = 6,    // skge_wide_kernel with a one-triangle symmetric operand
+    PLAN_SYMMETRIZE = 7,  // one-triangle operand expanded into a workspace, then the plain kernels
+};
+struct GemmPlan {
+    int kernel;
+    int splitk;
+    int64_t tiles;        // output tiles of the kernel
+    int64_t workgroups;   // tiles * splitk
+};
+GemmPlan plan_gemm_f64(const GemmProblem &p);
+GemmPlan plan_gemm_f32(const GemmProblem &p);
 
 // Expand a one-triangle operand (GemmProblem::tri conventions, n x n) into full storage
 // out[o*n + k] (skge_dense.hip); the fallback when the fused one-triangle kernel does not apply.

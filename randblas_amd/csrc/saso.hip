@@ -32,6 +32,10 @@
 
 namespace rbh {
 
+// which apply the calling thread's last sparse sketch ran (rbh_sparse_last_path)
+static thread_local int g_sparse_path = SPARSE_PATH_NONE;
+int sparse_last_path() { return g_sparse_path; }
+
 constexpr int SP_KC = 128;        // contracted indices per chunk (LDS panel depth), section 2
 
 // ------------------------------------------------------------------------------------------
@@ -565,9 +569,6 @@ constexpr int SU_LDP = SP_KC + 1;             // panel column stride (elements)
 #endif
 constexpr int SU_D = SU_D_DEF;                // entries per walk step
 constexpr int SU_WIN = 64 - 2 * SU_D;         // records per register window
-#ifndef SU_ABL
-#define SU_ABL 0   // diagnostics only: 1 skips the walk, 4 the panel loads, 8 static-row updates, 16 no walk reads
-#endif
 // record: bits 0-5 accumulator register index (2 x row for f64, row for f32; s_set_gpr_idx_on reads
 // bits 0-7), bits 8-27 panel byte offset of k % SP_KC, bit 31 the sign of the value
 template <typename T> __host__ __device__ constexpr uint32_t su_pad() { return 0x80000000u | ((uint32_t)(SP_KC * sizeof(T)) << 8); }
@@ -662,7 +663,6 @@ template <> struct SuAcc<double> {
         uint32_t m;   // sign mask made opaque, so the xor is not fused into a v_bitop3 (see SuAcc<float>)
         asm("s_and_b32 %0, %1, 0x80000000" : "=s"(m) : "s"(rec) : "scc");   // (writes SCC)
         const double ys = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, y) ^ ((uint64_t)m << 32));
-        if (SU_ABL & 8) { a[0] += ys; return; }   // diagnostics: static row
         asm volatile("s_waitcnt lgkmcnt(0)\n\t"
                      "s_set_gpr_idx_on %2, gpr_idx(SRC0,DST)\n\t"
                      "s_nop 0\n\t"   // M0 -> indexed VALU wait state (see below)
@@ -680,7 +680,6 @@ template <> struct SuAcc<float> {
     __device__ __forceinline__ void set(int r, float x) { a[r] = x; }
     // The sign flip is inside the asm, from a scalar mask.
     __device__ __forceinline__ void add_at(uint32_t rec, float y) {
-        if (SU_ABL & 8) { a[0] += __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, y) ^ (rec & 0x80000000u)); return; }
         float t;
         asm volatile("v_xor_b32 %1, %3, %4\n\t"
                      "s_waitcnt lgkmcnt(0)\n\t"
@@ -806,7 +805,7 @@ __global__ __launch_bounds__(SU_NT) void saso_unit_kernel(const SparseApply p, c
     // records first: the store's wait for the panel then covers them, so no load from before the
     // loop is still counted in flight at its head (which made the first walk wait for every load)
     uint32_t rc_c = load_recs(bd_c);
-    if (!(SU_ABL & 4)) su_panel_load<T, YJ>(st, okm, p, 0, j0, tid);
+    su_panel_load<T, YJ>(st, okm, p, 0, j0, tid);
     su_panel_store<T, YJ>(st, okm, lds, c, tid);
     asm volatile("" ::"v"(rc_c));   // (the scheduler may still issue it last: wait for it here)
     __syncthreads();
@@ -817,7 +816,7 @@ __global__ __launch_bounds__(SU_NT) void saso_unit_kernel(const SparseApply p, c
         int bd_nn = bd_n;
         if (more) {
             rc_n = load_recs(bd_n);
-            if (!(SU_ABL & 4)) su_panel_load<T, YJ>(st, okm, p, ch + 1, j0, tid);
+            su_panel_load<T, YJ>(st, okm, p, ch + 1, j0, tid);
             if (ch + 2 < nchunks) bd_nn = load_bounds(ch + 2);
         }
         const uint32_t lanex = lane0 + (uint32_t)((ch & 1) * G::PANEL * sizeof(T));
@@ -830,8 +829,7 @@ __global__ __launch_bounds__(SU_NT) void saso_unit_kernel(const SparseApply p, c
 #pragma unroll
                 for (int q = 0; q < SU_D; ++q) {
                     w[q] = (uint32_t)__builtin_amdgcn_readlane((int)rc, x0 + q);
-                    if (SU_ABL & 16) y[q] = (T)(w[q] >> 8);   // diagnostics: no LDS read
-                    else y[q] = *reinterpret_cast<const T *>(lbase + lanex + ((w[q] >> 8) & 0xfffffu));
+                    y[q] = *reinterpret_cast<const T *>(lbase + lanex + ((w[q] >> 8) & 0xfffffu));
                 }
             };
             auto update = [&](const T (&y)[SU_D], const uint32_t (&w)[SU_D]) {
@@ -859,7 +857,7 @@ __global__ __launch_bounds__(SU_NT) void saso_unit_kernel(const SparseApply p, c
         // then was written to the wrong registers (lost panel elements, corrupted addresses). So
         // the next chunk's loads complete here.
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (!(SU_ABL & 1) && ne > 0) {
+        if (ne > 0) {
             // the first window comes from registers loaded a chunk ahead; a range longer than one
             // window (SU_WIN entries in 32 rows of one chunk, rare at C3) continues in windows
             // loaded here. The two are separate code paths, so the common one never waits on the
@@ -1061,14 +1059,6 @@ template <int N>
 __device__ __forceinline__ void sd_top(sd_u32x8 &r0, sd_u32x8 &r1, sd_u32x8 &r2, sd_u32x8 &r3, sd_u32x8 &r4,
                                        sd_u32x8 &r5, const uint32_t *rec) {
     static_assert(N >= 0 && N < 64, "vmcnt range");
-#ifdef SD_ABLATE_REC   // diagnostic build (wrong results, timing only): no record loads per chunk
-    asm volatile("s_waitcnt vmcnt(%7)\n\t"
-                 "s_barrier\n\t"
-                 "s_waitcnt lgkmcnt(0)"
-                 : "+s"(r0), "+s"(r1), "+s"(r2), "+s"(r3), "+s"(r4), "+s"(r5)
-                 : "s"(rec), "n"(N)
-                 : "memory");
-#else
     asm volatile("s_load_dwordx8 %0, %6, 0x0\n\t"
                  "s_load_dwordx8 %1, %6, 0x20\n\t"
                  "s_load_dwordx8 %2, %6, 0x40\n\t"
@@ -1081,23 +1071,13 @@ __device__ __forceinline__ void sd_top(sd_u32x8 &r0, sd_u32x8 &r1, sd_u32x8 &r2,
                  : "=&s"(r0), "=&s"(r1), "=&s"(r2), "=&s"(r3), "=&s"(r4), "=&s"(r5)
                  : "s"(rec), "n"(N)
                  : "memory");
-#endif
 }
 
-#ifdef SD_PROF
-// Diagnostic build only (-DSD_PROF, tools/build_var.sh + tools/saso_prof.py): per-phase cycle
-// totals of the DMA apply, summed over waves: 1 record load + barrier, 2 copy issue, 3 bounds,
-// 4 later record windows, 5 walk; 6 entries, 7 wave-chunks.
-__device__ unsigned long long rbh_sd_prof[16];   // [0, 8): copying waves, [8, 16): the others
-#define SD_T(slot) do { const uint64_t now_ = clock64(); pf[slot] += now_ - pf_t; pf_t = now_; } while (0)
-#else
-#define SD_T(slot) do { } while (0)
-#endif
 
 template <bool YJ, bool BUF>
 __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, const int32_t *seg,
-                                                         const uint32_t *rec32, int64_t nchunks, int64_t nrb,
-                                                         int vec_out) {
+                                                         const uint32_t *rec32, int32_t rec_lim, int64_t nchunks,
+                                                         int64_t nrb, int vec_out, const uint32_t *bad) {
     typedef double T;
     typedef SdCfg G;
     constexpr int KC = SD_KC;
@@ -1213,25 +1193,18 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     asm volatile("" : "+v"(sgn));
     const uint32_t lanebase = YJ ? lane * (uint32_t)sizeof(T)
                                  : (SD_PAD8 ? lane * (uint32_t)G::CSTR : lane * (uint32_t)(KC * sizeof(T)) + 16u * (lane & 15u));
-#ifdef SD_PROF
-    uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t pf_t = clock64();
-#endif
-    // A wave's records of chunk ch: rec32[gofs, gofs + ne), ne a multiple of 4; bounds in slot ch & 3
+    // A wave's records of chunk ch: rec32[gofs, gofs + ne), ne a multiple of 4; bounds in slot ch & 3.
+    // Both are clamped to the record array (rec_lim = its length less the window overrun), so even
+    // a bounds slot read while it is rewritten cannot send the scalar loads outside it.
     auto chunk_range = [&](int64_t ch, int &gofs, int &ne) {
         const int32_t *bb = bnd + (ch & (SD_BR - 1)) * 64;
         gofs = __builtin_amdgcn_readfirstlane(bb[wave]);
-        ne = __builtin_amdgcn_readfirstlane(bb[wave + 1]) - gofs;
-#ifdef SD_PROF
-        SD_T(3);
-        pf[6] += ne > 0 ? ne : 0;
-        pf[7] += 1;
-#endif
+        const int gend = __builtin_amdgcn_readfirstlane(bb[wave + 1]);
+        gofs = gofs < 0 ? 0 : (gofs > rec_lim ? rec_lim : gofs);
         // a sampled operator has no duplicate (row, k): at most SU_R * KC entries per wave
-        ne = ne < 0 ? 0 : (ne > SU_R * KC ? SU_R * KC : ne);
-#ifdef SD_ABLATE_WALK
-        ne = 0;   // diagnostic build: no walk
-#endif
+        const int most = rec_lim - gofs < SU_R * KC ? rec_lim - gofs : SU_R * KC;
+        ne = gend - gofs;
+        ne = ne < 0 ? 0 : (ne > most ? most : ne);
     };
     // Records come straight from HBM/L2 into SGPRs (scalar loads), SD_SW at a time. The loads and
     // their wait are one asm statement, so no SGPR destination is visible to the compiler before the
@@ -1293,7 +1266,6 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
                              : "=&s"(r0), "=&s"(r1), "=&s"(r2), "=&s"(r3), "=&s"(r4), "=&s"(r5)
                              : "s"(rec32 + gofs + done)
                              : "memory");
-            SD_T(4);
             uint32_t wr[SD_SW];
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
@@ -1301,18 +1273,16 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
                 wr[24 + q] = r3[q]; wr[32 + q] = r4[q]; wr[40 + q] = r5[q];
             }
             walk(wr, ne - done < SD_SW ? ne - done : SD_SW);
-            SD_T(5);
         }
     };
 
-    // Copy slot s (s < nchunks): the record bounds of chunk s + 1 (wave 0; clamped at the last
-    // chunk, so every slot has the same instruction count) and the panel of chunk s. Slot s is
-    // issued SD_PD chunks ahead of its walk, into the buffer chunk s - SD_NB last used.
+    // Copy slot s (s < nchunks): the record bounds of chunk s + 1 (wave 0) and the panel of chunk
+    // s. Slot s is issued SD_PD chunks ahead of its walk, into the buffer chunk s - SD_NB last used.
+    // The last slot has no bounds to copy; with SD_PD > 1 (counted vmcnt waits) it re-copies the
+    // last chunk's (unchanged) bounds so every slot has the same instruction count.
     auto issue_slot = [&](int64_t s) {
-        dma_bounds(s + 1 < nchunks ? s + 1 : nchunks - 1);
-#ifndef SD_ABLATE_COPY   // diagnostic build: no copies
+        if (SD_PD > 1 || s + 1 < nchunks) dma_bounds(s + 1 < nchunks ? s + 1 : nchunks - 1);
         dma_panel(s);
-#endif
     };
     dma_bounds(0);
     wait_vm<0>();
@@ -1320,17 +1290,7 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     int gofs = 0, ne = 0;
     if (nchunks > 0) chunk_range(0, gofs, ne);
     for (int64_t s = 0; s < SD_PD && s < nchunks; ++s) issue_slot(s);
-#ifdef SD_ABLATE_REC   // diagnostic build: every chunk walks chunk 0's first window (valid records)
-    asm volatile(SD_LOADS "s_waitcnt lgkmcnt(0)"
-                 : "=&s"(r0), "=&s"(r1), "=&s"(r2), "=&s"(r3), "=&s"(r4), "=&s"(r5)
-                 : "s"(rec32 + gofs)
-                 : "memory");
-#endif
-#ifdef SD_ABLATE_COPY
-    constexpr int NIW = 0;
-#else
     constexpr int NIW = NI;
-#endif
     for (int64_t ch = 0; ch < nchunks; ++ch) {
         // this wave's copies of slot ch (panel ch, bounds ch + 1) have landed once at most the
         // slots issued after it are in flight (in-order vmcnt), then the barrier makes every
@@ -1341,20 +1301,18 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
         } else {
             sd_top<0>(r0, r1, r2, r3, r4, r5, rec32 + gofs);
         }
-        SD_T(1);
         const int gofs_c = gofs, ne_c = ne;
         if (ch + 1 < nchunks) chunk_range(ch + 1, gofs, ne);   // bounds ch + 1: visible since this barrier
         if (ch + SD_PD < nchunks) issue_slot(ch + SD_PD);
-        SD_T(2);
         walk_chunk(ch, gofs_c, ne_c);
     }
 #undef SD_LOADS
-#ifdef SD_PROF
-    if (lane == 0)
-        for (int q = 0; q < 8; ++q) atomicAdd(&rbh_sd_prof[q + (wave < SD_CW ? 0 : 8)], (unsigned long long)pf[q]);
-#endif
     wait_vm<0>();
     __syncthreads();   // the epilogue reuses the panel memory
+    if (bad && *bad) {   // the caller's arrays failed mark_check_kernel's test: fail loudly
+#pragma unroll
+        for (int r = 0; r < SU_R; ++r) acc.set(r, __builtin_nan(""));
+    }
     su_epilogue<T>(acc, reinterpret_cast<T *>(smem), p, row0, j0, wave, lane, vec_out);
 }
 
@@ -1401,6 +1359,22 @@ __global__ void mark_kernel(int64_t nnz, const int64_t *rows, const int64_t *col
     int64_t v, i;
     uint32_t kk;
     if (e < nnz && sp_locate(e, rows, cols, p, v, kk, i)) atomicOr(&mask[(v << (p.kcs - 5)) + kk / 32], 1u << (kk % 32));
+}
+
+// mark_kernel for the caller's arrays, checking what the LDS-DMA apply assumes: every in-window value
+// alpha * v is +-1 exactly (bit 0 of *bad otherwise) and no (row, k) repeats (bit 1: the mark was
+// already set)
+__global__ void mark_check_kernel(int64_t nnz, const int64_t *rows, const int64_t *cols, const double *vals,
+                                  const SparseApply p, uint32_t *mask, uint32_t *bad) {
+    const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    int64_t v, i;
+    uint32_t kk;
+    if (e >= nnz || !sp_locate(e, rows, cols, p, v, kk, i)) return;
+    const double x = p.alpha * vals[e];
+    uint32_t f = (x == 1.0 || x == -1.0) ? 0u : 1u;
+    const uint32_t bit = 1u << (kk % 32);
+    if (atomicOr(&mask[(v << (p.kcs - 5)) + kk / 32], bit) & bit) f |= 2u;
+    if (f) atomicOr(bad, f);
 }
 
 // records of segment g = (chunk, group of SU_R rows: one wave's rows), padded to a multiple of 4
@@ -1492,8 +1466,11 @@ __global__ void place_kernel(int64_t nnz, const int64_t *rows, const int64_t *co
 }
 
 // The LDS-DMA apply (section 5) on a sort-free CSR. With gen, the operator is sampled here into
-// the workspace and its entries marked in the same pass (fill_sparse_small_kernel<.., true>).
-// hipErrorNotSupported (nothing done): too many records for int32 offsets.
+// the workspace and its entries marked in the same pass (fill_sparse_small_kernel<.., true>);
+// otherwise the caller's arrays are marked and checked (mark_check_kernel): with
+// p.arrays_filled == 0 the host waits for the check and returns hipErrorNotSupported when it
+// fails, with 1 the apply reads the check's flag itself.
+// hipErrorNotSupported (nothing written to C): too many records for int32 offsets, or the check failed.
 static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, const int64_t *rows, const int64_t *cols,
                                  const double *vals, int64_t nnz, bool y_k, hipStream_t s) {
     static_assert(SD_KC >= 32, "whole mask words per virtual row");
@@ -1517,7 +1494,8 @@ static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, co
     if (err != hipSuccess) return err;
     const size_t gen_bytes = gen ? n * (2 * sizeof(int64_t) + sizeof(double)) + 64 : 0;
     const size_t bytes = (size_t)NV * 4 * mw + (size_t)NGT * sizeof(int32_t) + (size_t)NV * sizeof(int32_t) +
-                         (size_t)(NGT + 1) * sizeof(int32_t) + nrec * sizeof(uint32_t) + scan_bytes + gen_bytes + 512;
+                         (size_t)(NGT + 1) * sizeof(int32_t) + nrec * sizeof(uint32_t) + scan_bytes + gen_bytes + 512 +
+                         16;
     char *ws = nullptr;
     err = ws_alloc((void **)&ws, bytes, s);
     if (err != hipSuccess) return err;
@@ -1530,6 +1508,7 @@ static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, co
     int32_t *seg = (int32_t *)carve((size_t)(NGT + 1) * sizeof(int32_t));
     uint32_t *rec = (uint32_t *)carve(nrec * sizeof(uint32_t));
     void *tmp = carve(scan_bytes);
+    uint32_t *bad = gen ? nullptr : (uint32_t *)carve(sizeof(uint32_t));
     if (gen) {
         int64_t *gr = (int64_t *)carve(n * sizeof(int64_t));
         int64_t *gc = (int64_t *)carve(n * sizeof(int64_t));
@@ -1538,11 +1517,22 @@ static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, co
     }
     const uint32_t kmul = y_k ? (uint32_t)sizeof(double) : (uint32_t)(SU_J * sizeof(double));
     err = hipMemsetAsync(mask, 0, mask_b, s);
+    if (err == hipSuccess && bad) err = hipMemsetAsync(bad, 0, sizeof(uint32_t), s);
     if (err == hipSuccess && gen) {
         err = launch_fill_sparse_t<double>(*gen, (int64_t *)rows, (int64_t *)cols, (double *)vals, s, &p, mask);
     } else if (err == hipSuccess && nnz > 0) {
-        hipLaunchKernelGGL(mark_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, rows, cols, p, mask);
+        hipLaunchKernelGGL(mark_check_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, rows, cols,
+                           vals, p, mask, bad);
         err = hipGetLastError();
+    }
+    if (err == hipSuccess && bad && !p.arrays_filled) {   // arrays of unknown origin: wait for the check
+        uint32_t h = 0;
+        err = hipMemcpyAsync(&h, bad, sizeof(h), hipMemcpyDeviceToHost, s);
+        if (err == hipSuccess) err = hipStreamSynchronize(s);
+        if (err == hipSuccess && h != 0) {
+            (void)ws_free(ws, s);
+            return hipErrorNotSupported;
+        }
     }
     if (err == hipSuccess && NGT > 0) {
         hipLaunchKernelGGL(seg_rows_kernel, dim3((unsigned)((NGT * SU_R + 255) / 256)), dim3(256), 0, s, NGT, NG, p.M,
@@ -1563,22 +1553,24 @@ static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, co
         err = hipGetLastError();
     }
     if (err == hipSuccess) {
+        g_sparse_path = SPARSE_PATH_DMA;
         timing_begin(s);
         const int64_t nrb_u = (p.M + SU_ROWS - 1) / SU_ROWS;
         const dim3 grid_u((unsigned)(((p.N + SU_J - 1) / SU_J) * nrb_u));
         const int vec_out = p.crs == 1 && (p.ccs % 2) == 0 && (((uintptr_t)p.C) % 16) == 0;
         // buffer-resource copies when a column tile (64 columns to K) spans less than 2^31 bytes
         const bool buf = y_k && ((int64_t)SU_J * p.ysj + p.K) * (int64_t)sizeof(double) < ((int64_t)1 << 31);
-#ifdef SD_NO_BUF   // diagnostic build: global-address copies only
-        const bool use_buf = false;
-#else
         const bool use_buf = buf;
-#endif
+        const int32_t rec_lim = (int32_t)(nrec - 256);   // the walk's windows read up to 255 records past an end
+        const uint32_t *chk = bad;   // the kernel reads the check's flag (null: sampled here, nothing to check)
         if (y_k && use_buf)
-            hipLaunchKernelGGL((saso_dma_kernel<false, true>), grid_u, dim3(SU_NT), 0, s, p, seg, rec, nchunks, nrb_u, vec_out);
+            hipLaunchKernelGGL((saso_dma_kernel<false, true>), grid_u, dim3(SU_NT), 0, s, p, seg, rec, rec_lim, nchunks,
+                               nrb_u, vec_out, chk);
         else if (y_k)
-            hipLaunchKernelGGL((saso_dma_kernel<false, false>), grid_u, dim3(SU_NT), 0, s, p, seg, rec, nchunks, nrb_u, vec_out);
-        else hipLaunchKernelGGL((saso_dma_kernel<true, false>), grid_u, dim3(SU_NT), 0, s, p, seg, rec, nchunks, nrb_u, vec_out);
+            hipLaunchKernelGGL((saso_dma_kernel<false, false>), grid_u, dim3(SU_NT), 0, s, p, seg, rec, rec_lim, nchunks,
+                               nrb_u, vec_out, chk);
+        else hipLaunchKernelGGL((saso_dma_kernel<true, false>), grid_u, dim3(SU_NT), 0, s, p, seg, rec, rec_lim, nchunks,
+                                nrb_u, vec_out, chk);
         err = hipGetLastError();
         timing_end(s);
     }
@@ -1586,28 +1578,17 @@ static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, co
     return err != hipSuccess ? err : e2;
 }
 
-#ifdef SD_PROF
-extern "C" int rbh_diag_saso_prof(unsigned long long *out, int reset) {
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rbh_sd_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
-    if (reset) {
-        unsigned long long z[16] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(rbh_sd_prof), z, sizeof(z)) != hipSuccess) return -1;
-    }
-    return 0;
-}
-#endif
-
-// The DMA kernel's conditions: f64, values +-1 (sampled operator: distinct entries), |alpha| = 1
-// (the panel is Y itself), Y contiguous along k or j in 16-B vectors.
-static bool dma_eligible(const SparseApply &p, bool &y_k) {
+// The DMA kernel's layout conditions: Y contiguous along k or j in 16-B vectors (f64).
+static bool dma_layout_ok(const SparseApply &p, bool &y_k) {
     constexpr int VEC = 2;
     y_k = p.ysk == 1 && (p.ysj % VEC) == 0 && (((uintptr_t)p.Y) % 16) == 0 && (p.K % VEC) == 0;
     const bool y_jd = p.ysj == 1 && (p.ysk % VEC) == 0 && (((uintptr_t)p.Y) % 16) == 0 && (p.N % VEC) == 0;
-#ifdef SD_NO_DMA   // diagnostic build: the register-staged unit kernel takes these calls
-    return false;
-#endif
-    return p.unit_vals && (p.alpha == 1.0 || p.alpha == -1.0) && (y_k || y_jd);
+    return y_k || y_jd;
+}
+// ... for an operator sampled in the call (values +-1, distinct entries): also |alpha| = 1, so the
+// panel is Y itself
+static bool dma_eligible(const SparseApply &p, bool &y_k) {
+    return dma_layout_ok(p, y_k) && p.unit_vals && (p.alpha == 1.0 || p.alpha == -1.0);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1705,6 +1686,7 @@ static hipError_t run_sparse_gather(const SparseApply &p, const int64_t *rows, c
         err = launch_class_ptr(nnz, k_out, 32, p.M, rp, s);   // rp[i]: row i's first entry, rp[M] the valid count
     }
     if (err == hipSuccess) {
+        g_sparse_path = SPARSE_PATH_GATHER;
         timing_begin(s);
         const int64_t ncb = (p.N + GA_NT * GA_CPT - 1) / (GA_NT * GA_CPT);
         hipLaunchKernelGGL(saso_gather_kernel<T>, dim3((unsigned)(p.M * ncb)), dim3(GA_NT), 0, s, p, rp, k_out, v_out, ncb);
@@ -1718,13 +1700,18 @@ static hipError_t run_sparse_gather(const SparseApply &p, const int64_t *rows, c
 template <typename T>
 static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, const int64_t *cols, const T *vals,
                                      int64_t nnz, hipStream_t s) {
+    g_sparse_path = SPARSE_PATH_NONE;
     if (p.M <= 0 || p.N <= 0) return hipSuccess;
     if (nnz >= (int64_t)0x7fffffff) return hipErrorInvalidValue;
-    {   // LDS-DMA kernel (section 5) on the sort-free CSR (section 7)
+    {   // LDS-DMA kernel (section 5) on the sort-free CSR (section 7), for the caller's arrays when
+        // every in-window alpha * v is +-1 and no (row, k) repeats -- a fill_sparse output applied
+        // with |alpha| = 1, the reference's fill-once / apply-many use (skge.hh:503-504,
+        // sparse_skops.hh:389-413) -- which mark_check_kernel verifies on the device
         bool y_k;
-        if (sizeof(T) == 8 && dma_eligible(p, y_k)) {
+        const bool values_can_be_unit = !p.unit_vals || p.alpha == 1.0 || p.alpha == -1.0;
+        if (sizeof(T) == 8 && nnz > 0 && values_can_be_unit && dma_layout_ok(p, y_k)) {
             const hipError_t e = run_sparse_dma(p, nullptr, rows, cols, (const double *)vals, nnz, y_k, s);
-            if (e != hipErrorNotSupported) return e;   // NotSupported: too many records, nothing done
+            if (e != hipErrorNotSupported) return e;   // NotSupported: check failed / too many records
         }
     }
     {   // row gather (section 8) for very sparse operators over j-contiguous Y
@@ -1788,9 +1775,13 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
     static_assert(SP_KC == 128, "class shift 7");
     err = launch_class_ptr(nnz, k_out, 7, NV, vrp, s);
     if (err != hipSuccess) { (void)ws_free(ws, s); return err; }
-    if (nnz > 0)
+    if (nnz > 0) {
         hipLaunchKernelGGL(entry_rec_kernel<T>, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, k_out, v_out,
                            p.M, kl, rec, (uint32_t)sizeof(T));
+        err = hipGetLastError();
+        if (err != hipSuccess) { (void)ws_free(ws, s); return err; }
+    }
+    g_sparse_path = unit ? SPARSE_PATH_SORTED_UNIT : SPARSE_PATH_SORTED;   // (unit: exits for mixed values)
     timing_begin(s);
     if (unit) {
         const int64_t nrb_u = (p.M + SU_ROWS - 1) / SU_ROWS;
@@ -1819,6 +1810,7 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
 // operator is sampled into a workspace and takes the general apply.
 template <typename T>
 static hipError_t run_sparse_sampled_t(const SparseApply &p0, const SparseGen &g, int64_t nnz, hipStream_t s) {
+    g_sparse_path = SPARSE_PATH_NONE;
     if (nnz >= (int64_t)0x7fffffff) return hipErrorInvalidValue;   // int32 CSR offsets (as run_sparse_apply_t)
     SparseApply p = p0;
     p.unit_vals = 1;   // fill_sparse draws values +-1 (sparse_skops.hh:389-413)
@@ -1839,6 +1831,7 @@ static hipError_t run_sparse_sampled_t(const SparseApply &p0, const SparseGen &g
     int64_t *gc = gr + n;
     T *gv = (T *)(gc + n);
     err = launch_fill_sparse_t<T>(g, gr, gc, gv, s);
+    p.arrays_filled = 1;   // fill_sparse's own output: the apply need not wait for its check
     // left_spmm returns after the beta scaling when alpha == 0 (spmm_dispatch.hh:134-135)
     if (err == hipSuccess) err = run_sparse_apply_t<T>(p, gr, gc, gv, p.alpha == 0.0 ? 0 : nnz, s);
     hipError_t e2 = ws_free(ws, s);

@@ -27,6 +27,11 @@ struct SparseApply {
     int64_t crs, ccs;
     int unit_vals;   // every value is +1 or -1 (operator sampled by fill_sparse in this call)
     int kcs;         // LDS-DMA apply (saso.hip section 5): log2 of its chunk depth; set by the apply itself
+    // Caller's COO arrays (rbh_options.sparse_filled): 0 = of unknown origin -- the LDS-DMA apply
+    // takes them after a device check (every in-window alpha*v is +-1, no duplicate (row, k)) that
+    // the host waits for; 1 = fill_sparse's output for this operator, unmodified -- the same check
+    // runs on the device without a wait, and a failed check makes the apply write NaN.
+    int arrays_filled;
 };
 
 hipError_t launch_fill_sparse_f64(const SparseGen &g, int64_t *rows, int64_t *cols, double *vals, hipStream_t s);
@@ -39,6 +44,13 @@ hipError_t run_sparse_apply_f32(const SparseApply &p, const int64_t *rows, const
 // Sample the operator (SparseGen, nnz entries) on the device and apply it: C = beta*C + op'(S) Y.
 hipError_t run_sparse_sampled_f64(const SparseApply &p, const SparseGen &g, int64_t nnz, hipStream_t s);
 hipError_t run_sparse_sampled_f32(const SparseApply &p, const SparseGen &g, int64_t nnz, hipStream_t s);
+
+// The apply a sparse sketch ran (rbh_sparse_last_path): none (empty), the LDS-DMA kernel on the
+// sort-free CSR, the row gather, the sorted CSR with the uniform-value kernel (its general kernel
+// takes over for mixed values), or the general kernel.
+enum SparsePath : int { SPARSE_PATH_NONE = 0, SPARSE_PATH_DMA = 1, SPARSE_PATH_GATHER = 2, SPARSE_PATH_SORTED_UNIT = 3,
+                        SPARSE_PATH_SORTED = 4 };
+int sparse_last_path();
 
 // CSR/CSC pointer array (n_major + 1 entries) -> the major index of every entry (saso.hip).
 hipError_t launch_expand_ptr(int64_t n_major, const int64_t *ptr, int64_t *out, hipStream_t s);

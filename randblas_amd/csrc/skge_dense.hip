@@ -24,7 +24,6 @@
 //     row tiles that share one Y column panel run on one XCD and share its L2.
 #include "common.hpp"
 
-#include <cstdlib>
 #include <type_traits>
 
 namespace rbh {
@@ -1186,21 +1185,36 @@ static hipError_t launch_one(const GemmProblem &p, hipStream_t s) {
     return e;
 }
 
-constexpr int64_t SPLIT_TILES = 128;   // fewer output tiles than this: split K ...
-constexpr int64_t SPLIT_MIN_NK = 128;  // ... when K has at least this many steps (K >= 2048). A split
-                                       // sum rounds differently from the unsplit kernels (within the
-                                       // tolerance of every dense parity test); below this K every
+constexpr int64_t SPLIT_MIN_NK = 128;  // split K only when it has at least this many steps (K >= 2048).
+                                       // A split sum rounds differently from the unsplit kernels (within
+                                       // the tolerance of every dense parity test); below this K every
                                        // kernel adds in the same order, so layouts agree bitwise
 
-// split-K factor: 1, or enough splits to give 256 workgroups when the output tiles alone cannot
-// fill the chip (C1: d = 128, n = 4096, 16 wide tiles, split 16), each split keeping at least 16 K
-// steps; RBH_SPLITK = s forces s. Deterministic: the splits are added in order by the reduction.
-static int choose_split(int64_t tiles, int64_t nk) {
-    static const int split_env = [] { const char *e = getenv("RBH_SPLITK"); return e ? atoi(e) : 0; }();
+// compute units of the current device (one wide-kernel workgroup each)
+static int64_t device_cus() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (cus[dev] <= 0) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+        cus[dev] = c;
+    }
+    return cus[dev];
+}
+
+// split-K factor. req >= 1 (rbh_options.splitk): exactly req slices. req == 0: when the output tiles
+// fill at most half the chip, floor(CUs / tiles) slices -- every workgroup then runs at once (C1:
+// d = 128, n = 4096, 16 wide tiles, split 16; the north star's d = 256 rank shard at N = 8, 128 tiles,
+// split 2) -- each keeping at least 16 K steps; otherwise 1. Deterministic: the reduction adds the
+// slices in order. The slices depend only on (K, split), so a call whose columns are cut into
+// chunks gives the unchunked call's bits whenever every chunk uses the same split
+// (RowShardedSketch passes the whole rank problem's split, rbh_lskge3_plan).
+static int choose_split(int64_t tiles, int64_t nk, int req) {
     int split = 1;
-    if (split_env > 0) split = split_env;
-    else if (tiles < SPLIT_TILES && nk >= SPLIT_MIN_NK) {
-        const int64_t want = (256 + tiles - 1) / tiles, most = nk / 16;
+    if (req >= 1) split = req;
+    else if (tiles > 0 && 2 * tiles <= device_cus() && nk >= SPLIT_MIN_NK) {
+        const int64_t want = device_cus() / tiles, most = nk / 16;
         split = (int)(want < most ? want : most);
     }
     if (split > nk) split = (int)nk;
@@ -1218,7 +1232,7 @@ static hipError_t launch_fused(const GemmProblem &p, hipStream_t s) {
     // forms C. Measured at C4 (256 workgroups, one per CU): 6.08 ms unsplit, 6.11 / 6.14 ms with
     // 2 / 4 splits forced, so a full grid stays unsplit.
     const int64_t nk = (p.K + BK - 1) / BK;
-    const int split = choose_split(nb, nk);
+    const int split = choose_split(nb, nk, p.split_req);
     GemmProblem q = p;
     q.splitk = split;
     q.partial = nullptr;
@@ -1254,13 +1268,13 @@ static bool fused_ok(const GemmProblem &p) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Materialised generated operand (opt-in: RBH_MATERIALISE=1)
+// Materialised generated operand (opt-in: rbh_options.materialise = 1)
 // ------------------------------------------------------------------------------------------
 // By default the wide kernels draw their operator tile inside the GEMM, so the operator is never
 // written to memory (the north star). A drawing wide kernel regenerates every entry once per
 // 512-row tile of the memory operand (n / 512 = 32 times at C2), and on gfx950 an f64 / f32-input
 // MFMA holds its SIMD's issue for its whole duration (tools/micro/mfma_coexec.hip), so that draw's
-// VALU work adds to the MFMA time instead of hiding under it. With RBH_MATERIALISE=1 the launcher
+// VALU work adds to the MFMA time instead of hiding under it. With materialise = 1 the launcher
 // instead does what the reference does (fill_dense of submat(S), then GEMM, skge.hh:173-215):
 // gen_fill_kernel draws the window once into a workspace, gmat[o * K + k], and the wide kernel
 // loads its tile from there (GMAT). The LDS image and the MFMA order are unchanged, so the results
@@ -1301,8 +1315,7 @@ __global__ __launch_bounds__(256) void gen_fill_kernel(const GenOperand g, int64
 // draws in place (the default; few memory tiles, too large, or no workspace)
 template <typename T, int GK, int FAMILY, bool GX>
 static hipError_t materialise(const GemmProblem &p, void **buf, hipStream_t s) {
-    const char *env = getenv("RBH_MATERIALISE");   // read per call (a caller may switch it)
-    const bool on = env && env[0] == '1';
+    const bool on = p.materialise != 0;   // rbh_options.materialise
     *buf = nullptr;
     const int64_t gnO = GX ? p.M : p.N, mnO = GX ? p.N : p.M;
     const int64_t bytes = gnO * p.K * (int64_t)sizeof(T);
@@ -1329,7 +1342,7 @@ static hipError_t launch_wide(const GemmProblem &p, hipStream_t s) {
     const int64_t gnO = GX ? p.M : p.N, mnO = GX ? p.N : p.M;
     const int64_t nb = ((gnO + 63) / 64) * ((mnO + 511) / 512);
     if (nb <= 0) return hipSuccess;
-    const int split = choose_split(nb, p.K / BK);
+    const int split = choose_split(nb, p.K / BK, p.split_req);
     GemmProblem q = p;
     q.splitk = split;
     q.partial = nullptr;
@@ -1388,7 +1401,7 @@ static hipError_t launch_wide32(const GemmProblem &p, hipStream_t s) {
     const int64_t nb = ((gnO + 63) / 64) * ((mnO + 511) / 512);
     if (nb <= 0) return hipSuccess;
     // split-K on the same terms as the 16-deep kernels (the split counts 16-deep steps)
-    const int split = choose_split(nb, p.K / BK);
+    const int split = choose_split(nb, p.K / BK, p.split_req);
     GemmProblem q = p;
     q.splitk = split;
     q.partial = nullptr;
@@ -1433,10 +1446,7 @@ static bool wide32_ok(const GemmProblem &p) {
     return sizeof(T) == 4 && fused_ok(p) && p.K % KB32 == 0 && wide_offsets_ok<T>(p);
 }
 
-// One-triangle symmetric memory operand: the wide f64 kernel when the generated operand runs its
-// counter along k from a Philox quad (GEN_OK, every MajorAxis::Long operator) and K % 16 == 0; full
-// storage also needs 16-B aligned rows. Otherwise hipErrorNotSupported, and the caller expands
-// the triangle (launch_symmetrize) and runs the plain kernels.
+// the wide kernel instantiated for one-triangle operand p.tri (1-4)
 template <int FAM, bool GX>
 static hipError_t launch_wide_tri(const GemmProblem &p, hipStream_t s) {
     switch (p.tri) {
@@ -1448,29 +1458,97 @@ static hipError_t launch_wide_tri(const GemmProblem &p, hipStream_t s) {
     return hipErrorInvalidValue;
 }
 
+// Can the wide f64 kernel take the one-triangle operand directly (launch_gemm_tri)?
 template <typename T>
-static hipError_t launch_gemm_tri(const GemmProblem &p, hipStream_t s) {
-    if (sizeof(T) != 8 || (p.xkind == MEM) == (p.ykind == MEM)) return hipErrorNotSupported;
+static bool tri_ok(const GemmProblem &p) {
+    if (sizeof(T) != 8 || (p.xkind == MEM) == (p.ykind == MEM)) return false;
     const bool gx = p.xkind != MEM;
     const GenOperand &g = gx ? p.xg : p.yg;
     const MemOperand &m = gx ? p.ym : p.xm;
-    if ((gx ? p.xkind : p.ykind) != GEN_OK || (g.pc0 & 3) || p.K % BK) return hipErrorNotSupported;
-    if (p.tri <= 2 && ((((uintptr_t)m.ptr) % 16) || (m.so & 1))) return hipErrorNotSupported;
+    if ((gx ? p.xkind : p.ykind) != GEN_OK || (g.pc0 & 3) || p.K % BK) return false;
+    if (p.tri <= 2 && ((((uintptr_t)m.ptr) % 16) || (m.so & 1))) return false;
     // tiles inside the triangle take the plain 32-bit byte-offset loads
-    if (p.tri <= 2 && !wide_offsets_ok<double>(p)) return hipErrorNotSupported;
+    if (p.tri <= 2 && !wide_offsets_ok<double>(p)) return false;
     // 32-bit byte offsets into the whole stored triangle in the kernel
     const int64_t n = p.tri_n, last = p.tri <= 2 ? (n - 1) * m.so + n : n * (n + 1) / 2;
-    if (last * (int64_t)sizeof(double) >= ((int64_t)1 << 32)) return hipErrorNotSupported;
-    const bool unif = g.family == rb::UNIFORM;
+    return last * (int64_t)sizeof(double) < ((int64_t)1 << 32);
+}
+
+// One-triangle symmetric memory operand: the wide f64 kernel when the generated operand runs its
+// counter along k from a Philox quad (GEN_OK, every MajorAxis::Long operator) and K % 16 == 0; full
+// storage also needs 16-B aligned rows. Otherwise hipErrorNotSupported, and the caller expands
+// the triangle (launch_symmetrize) and runs the plain kernels.
+template <typename T>
+static hipError_t launch_gemm_tri(const GemmProblem &p, hipStream_t s) {
+    if (!tri_ok<T>(p)) return hipErrorNotSupported;
+    const bool gx = p.xkind != MEM;
+    const bool unif = (gx ? p.xg : p.yg).family == rb::UNIFORM;
     if (gx) return unif ? launch_wide_tri<rb::UNIFORM, true>(p, s) : launch_wide_tri<rb::GAUSSIAN, true>(p, s);
     return unif ? launch_wide_tri<rb::UNIFORM, false>(p, s) : launch_wide_tri<rb::GAUSSIAN, false>(p, s);
 }
+
+// Which kernel launch_gemm runs for p, with its tiles and split (the same tests, in the same order).
+template <typename T>
+static GemmPlan plan_gemm(const GemmProblem &p) {
+    GemmPlan pl{PLAN_NONE, 1, 0, 0};
+    if (p.M <= 0 || p.N <= 0) return pl;
+    if (p.K <= 0 || p.alpha == 0.0) { pl.kernel = PLAN_SCALE; return pl; }
+    auto wide_tiles = [&]() {
+        const bool gx = p.xkind != MEM;
+        const int64_t gnO = gx ? p.M : p.N, mnO = gx ? p.N : p.M;
+        return ((gnO + 63) / 64) * ((mnO + 511) / 512);
+    };
+    if (p.tri && !tri_ok<T>(p)) {   // expanded into full storage first, then planned as such
+        GemmProblem q = p;
+        q.tri = 0;
+        MemOperand &mo = q.xkind == MEM ? q.xm : q.ym;
+        int &mode = q.xkind == MEM ? q.xmode : q.ymode;
+        mo.so = p.tri_n;
+        mo.sk = 1;
+        mode = (p.K % (16 / (int)sizeof(T))) == 0 ? 2 : 1;   // the workspace is 256-B aligned, rows of n
+        if ((p.tri_n * (int64_t)sizeof(T)) % 16) mode = 1;
+        pl = plan_gemm<T>(q);
+        pl.kernel = PLAN_SYMMETRIZE;
+        return pl;
+    }
+    if (p.tri) {
+        pl.kernel = PLAN_WIDE_TRI;
+        pl.tiles = wide_tiles();
+        pl.splitk = choose_split(pl.tiles, p.K / BK, p.split_req);
+    } else if (wide_ok<T>(p)) {
+        pl.kernel = PLAN_WIDE;
+        pl.tiles = wide_tiles();
+        pl.splitk = choose_split(pl.tiles, p.K / BK, p.split_req);
+    } else if (wide32_ok<T>(p)) {
+        pl.kernel = PLAN_WIDE32;
+        pl.tiles = wide_tiles();
+        pl.splitk = choose_split(pl.tiles, p.K / BK, p.split_req);
+    } else if (fused_ok(p)) {
+        constexpr bool F32 = sizeof(T) == 4;
+        constexpr int64_t TG = F32 ? 64 : 128, TMW = F32 ? 512 : 256;
+        const bool gx = p.xkind != MEM;
+        const int64_t BM = gx ? TG : TMW, BN = gx ? TMW : TG;
+        pl.kernel = PLAN_FUSED;
+        pl.tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+        pl.splitk = choose_split(pl.tiles, (p.K + BK - 1) / BK, p.split_req);
+    } else {
+        const bool gen_y = p.xkind == MEM && p.ykind != MEM;
+        const int64_t BM = gen_y ? 256 : 128, BN = gen_y ? 128 : 256;
+        pl.kernel = PLAN_GENERIC;
+        pl.tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+    }
+    pl.workgroups = pl.tiles * pl.splitk;
+    return pl;
+}
+GemmPlan plan_gemm_f64(const GemmProblem &p) { return plan_gemm<double>(p); }
+GemmPlan plan_gemm_f32(const GemmProblem &p) { return plan_gemm<float>(p); }
 
 template <typename T>
 static hipError_t launch_gemm(const GemmProblem &p, hipStream_t s) {
     if (p.tri) return launch_gemm_tri<T>(p, s);
     const bool unif = (p.xkind != MEM ? p.xg.family : p.yg.family) == rb::UNIFORM;
-    if (wide_ok<T>(p)) {
+    const int kernel = plan_gemm<T>(p).kernel;
+    if (kernel == PLAN_WIDE) {
 #define RBH_WIDE_L(GK, GX)                                                                     \
     return unif ? launch_wide<GK, rb::UNIFORM, GX>(p, s) : launch_wide<GK, rb::GAUSSIAN, GX>(p, s)
         if (p.xkind == GEN_OK) { RBH_WIDE_L(GEN_OK, true); }
@@ -1479,7 +1557,7 @@ static hipError_t launch_gemm(const GemmProblem &p, hipStream_t s) {
         if (p.ykind == GEN_OO) { RBH_WIDE_L(GEN_OO, false); }
 #undef RBH_WIDE_L
     }
-    if (wide32_ok<T>(p)) {
+    if (kernel == PLAN_WIDE32) {
 #define RBH_WIDE32_L(GK, GX)                                                                   \
     return unif ? launch_wide32<GK, rb::UNIFORM, GX>(p, s) : launch_wide32<GK, rb::GAUSSIAN, GX>(p, s)
         if (p.xkind == GEN_OK) { RBH_WIDE32_L(GEN_OK, true); }
@@ -1488,8 +1566,8 @@ static hipError_t launch_gemm(const GemmProblem &p, hipStream_t s) {
         if (p.ykind == GEN_OO) { RBH_WIDE32_L(GEN_OO, false); }
 #undef RBH_WIDE32_L
     }
-    if (fused_ok(p)) {
-        // tile (generated x memory outer indices) and waves; f32 variants selectable for tuning
+    if (kernel == PLAN_FUSED) {
+        // tile (generated x memory outer indices) and waves
 // f32 (where the 32-deep wide kernel does not apply): 64 generated x 512 memory rows, one wave
 // along the generated dimension. Each operator entry is drawn once per 512 memory columns instead of
 // 256, for the same 64 accumulators per lane. Measured at C4 (d = 256 per GPU, m = n = 32768):

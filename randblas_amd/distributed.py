@@ -1,88 +1,52 @@
-"""Output-row sharded sketching across the GPUs of a node.
+"""Sharded sketching across the GPUs of a node.
 
 Entry (i, k) of a RandBLAS dense operator is a pure function of (seed, i, k), and a SparseSkOp's
 column k is a pure function of (seed, k) (RandBLAS/dense_skops.hh:109-162,
 RandBLAS/sparse_skops.hh:72-92; the reference's "reproducible submatrices",
-rtd/source/updates/index.rst:34). So rank g of G computes rows [g*d_loc, (g+1)*d_loc) of
-B = S * A by calling sketch_general with ro_s = g*d_loc -- no operator data moves -- and the only
-exchange is the all-gather that reassembles B. That all-gather is pipelined with the compute:
-A's columns are cut into `chunks`; chunk c's shard is all-gathered (RCCL over xGMI on GPU, gloo
-on CPU in tests) while chunk c+1 is computed, then unpacked into the ColMajor d x n result -- on
-the GPU by the library's HIP copy (rbh_unpack_shards, one pass over the gathered bytes), on CPU
-tensors (the gloo tests) by the equivalent strided torch copy.
+rtd/source/updates/index.rst:34). So
 
-Every rank's operator rows are regenerated inside its fused GEMM (the default dense path keeps S
-out of HBM), so cutting A's columns into chunks adds no operator traffic: a chunk's output tiles
-draw the S tiles they need exactly as the unchunked call's tiles would.
+  * dense (RowShardedSketch): rank g computes rows [g*d_loc, (g+1)*d_loc) of B = S * A by calling
+    sketch_general with ro_s = g*d_loc -- no operator data moves, A is replicated;
+  * SASO (ColumnShardedSketch): rank g owns columns [g*n_loc, (g+1)*n_loc) of A and B, samples the
+    same operator locally and reads only its own block of A;
 
-The per-shard compute is a callable so the same driver runs the HIP path (bench.py) and the CPU
-oracle (tests/test_distributed_cpu.py):  compute(ro_s, j0, j1, out)  writes the d_loc x (j1-j0)
-ColMajor shard  B[ro_s : ro_s + d_loc, j0 : j1]  into the 1-D tensor `out`.
+and the one exchange is the all-gather (RCCL over xGMI on GPU, gloo on CPU in the tests) that
+reassembles B on every rank, followed by a copy that places the gathered shards (on the GPU the
+library's HIP kernel rbh_unpack_shards, one pass over the gathered bytes; on CPU tensors the
+equivalent strided torch copy).
+
+Pipelining. A step's exchange runs on a side stream and overlaps the NEXT step's compute: step s
+computes into buffer slot s % 2, its all-gather is issued behind that compute (the collective's
+stream waits for it), and the unpack waits for the gather on the exchange stream. Step s + 2 reuses
+the slot only after step s's exchange has finished. Only the last step's exchange is left after
+the last compute; wait() (or a device synchronisation) joins it.
+
+Bitwise results. A rank's shard is one library call over all its columns by default (chunks = 1),
+so it is bit for bit the call a single GPU makes for those rows (and, while no split-K engages,
+for any world size: the wide kernels add each output element's k terms in an order that does not
+depend on the tile it sits in). With chunks > 1 the columns are cut into chunks, computed one
+after another on the compute stream, each all-gathered as soon as it is done; the compute callable
+must then use the split-K factor of the rank's WHOLE problem (dense_rank_compute does: the library's
+rbh_lskge3_plan), so the chunks give the unchunked call's bits. Where a rank's problem has so few
+output tiles that the automatic policy splits K (a split of floor(CUs / tiles) when the tiles fill
+at most half the chip), its sum is rounded differently from a world size that does not split --
+within the reference's bound, not bitwise.
+
+The per-shard compute is a callable so the same drivers run the HIP path (bench.py) and the CPU
+oracle (tests/test_distributed_cpu.py): RowShardedSketch's  compute(ro_s, j0, j1, out)  writes the
+d_loc x (j1-j0) ColMajor shard  B[ro_s : ro_s + d_loc, j0 : j1]  into the 1-D tensor `out`;
+ColumnShardedSketch's  compute(j0, j1, out)  writes the d x (j1-j0) ColMajor block of this rank's
+local columns j0 .. j1.
 
 The all-gather runs whenever a process group is initialised, a group of one included: that is how
 the one-GPU box drives RCCL together with the HIP path (tests/test_gpu_rccl.py).
-
-On the GPU the chunks are computed on two streams in turn. A chunk's grid is a fraction of the
-unchunked call's (C2: 128 workgroups of 512 for a quarter of the columns, on 256 CUs), so one chunk
-at a time would leave CUs idle; two in flight fill the chip, and each chunk's all-gather starts as
-soon as its own kernel ends.
 """
 from __future__ import annotations
 
-from typing import Callable, List, Optional
+from typing import Callable, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
-
-
-class _Streams:
-    """Compute streams for the chunks (CUDA tensors; None on CPU): chunk c runs on stream c % 2,
-    after whatever the caller's stream has queued (the previous step's unpack and gather waits).
-    With timing on, every call records three events on the caller's stream: start, compute done
-    (both streams joined), and done (every chunk gathered and unpacked), so a caller can split a
-    step into compute and the exchange that is left exposed after it."""
-
-    def __init__(self, device: torch.device, n: int = 2):
-        self.main = None
-        self.s = [torch.cuda.Stream(device) for _ in range(n)] if device.type == "cuda" else []
-        self.timing = False
-        self.marks: List = []   # (start, compute done, done) per call
-
-    def _event(self):
-        e = torch.cuda.Event(enable_timing=True)
-        e.record(self.main)
-        return e
-
-    def begin(self):
-        if self.s:
-            self.main = torch.cuda.current_stream(self.s[0].device)
-            if self.timing:
-                self.marks.append([self._event()])
-            for st in self.s:
-                st.wait_stream(self.main)
-
-    def ctx(self, c: int):
-        import contextlib
-        return torch.cuda.stream(self.s[c % len(self.s)]) if self.s else contextlib.nullcontext()
-
-    def end(self):
-        if self.s:
-            for st in self.s:
-                self.main.wait_stream(st)
-            if self.timing:
-                self.marks[-1].append(self._event())
-
-    def done(self):
-        if self.s and self.timing:
-            self.marks[-1].append(self._event())
-
-    def split_ms(self):
-        """Mean (compute, exposed exchange) milliseconds per timed call (after a synchronize)."""
-        if not self.marks:
-            return None, None
-        comp = sum(a.elapsed_time(b) for a, b, _ in self.marks) / len(self.marks)
-        exch = sum(b.elapsed_time(c) for _, b, c in self.marks) / len(self.marks)
-        return comp, exch
 
 
 def _unpack(src: torch.Tensor, nshards: int, rows: int, run: int, dst: torch.Tensor, row_stride: int,
@@ -98,105 +62,170 @@ def _unpack(src: torch.Tensor, nshards: int, rows: int, run: int, dst: torch.Ten
     view.copy_(src[:nshards * rows * run].view(nshards, rows, run))
 
 
-class RowShardedSketch:
-    def __init__(self, d_total: int, n: int, compute: Callable[[int, int, int, torch.Tensor], None],
-                 dtype: torch.dtype, device: torch.device, chunks: int = 4, group=None):
+def _column_chunks(n: int, chunks: int) -> List[Tuple[int, int]]:
+    chunks = max(1, min(chunks, n))
+    bounds = [round(i * n / chunks) for i in range(chunks + 1)]
+    return [(bounds[i], bounds[i + 1]) for i in range(chunks) if bounds[i + 1] > bounds[i]]
+
+
+class _Pipeline:
+    """Buffers, streams and the per-step timing shared by both drivers. A subclass gives the column
+    chunks, the shard size per chunk, the compute call and the unpack geometry."""
+
+    SLOTS = 2
+
+    def __init__(self, cols: List[Tuple[int, int]], shard_elems: Callable[[int], int], dtype: torch.dtype,
+                 device, group):
         self.group = group
         self.dist = dist.is_initialized()   # gather through the group (RCCL / gloo), even a group of one
         self.world = dist.get_world_size(group) if self.dist else 1
         self.rank = dist.get_rank(group) if self.dist else 0
-        if d_total % self.world:
-            raise ValueError(f"d_total={d_total} is not divisible by the world size {self.world}")
+        self.cols = cols
+        device = torch.device(device)
+        self.cuda = device.type == "cuda"
+        self.local = [[torch.empty(shard_elems(j1 - j0), dtype=dtype, device=device) for j0, j1 in cols]
+                      for _ in range(self.SLOTS)]
+        self.gathered = [[torch.empty(self.world * shard_elems(j1 - j0), dtype=dtype, device=device)
+                          for j0, j1 in cols] for _ in range(self.SLOTS)] if self.dist else None
+        self.xs = torch.cuda.Stream(device) if self.cuda else None   # exchange (unpack) stream
+        self.slot_free: List[Optional[torch.cuda.Event]] = [None] * self.SLOTS
+        self.steps = 0
+        # timing (CUDA only): per step (start, compute done) on the compute stream
+        self.timing = False
+        self.marks: List = []
+
+    def _ev(self, stream):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(stream)
+        return e
+
+    def _compute(self, c: int, j0: int, j1: int, out: torch.Tensor) -> None:
+        raise NotImplementedError
+
+    def _unpack_chunk(self, c: int, j0: int, j1: int, src: torch.Tensor, B_full: torch.Tensor) -> None:
+        raise NotImplementedError
+
+    def __call__(self, B_full: Optional[torch.Tensor]) -> None:
+        """Enqueue one step: compute this rank's shard; with B_full, all-gather and reassemble the
+        whole sketch into it on every rank (on the exchange stream, overlapping the next step).
+        CPU tensors: synchronous."""
+        slot = self.steps % self.SLOTS
+        self.steps += 1
+        main = torch.cuda.current_stream(self.xs.device) if self.cuda else None
+        if self.cuda and self.slot_free[slot] is not None:
+            main.wait_event(self.slot_free[slot])   # step - 2's exchange has released the slot
+        if self.cuda and self.timing:
+            self.marks.append([self._ev(main)])
+        works = []
+        for c, (j0, j1) in enumerate(self.cols):
+            self._compute(c, j0, j1, self.local[slot][c])
+            if self.dist and B_full is not None:   # issued behind this chunk's compute
+                works.append(dist.all_gather_into_tensor(self.gathered[slot][c], self.local[slot][c],
+                                                         group=self.group, async_op=True))
+        if self.cuda and self.timing:
+            self.marks[-1].append(self._ev(main))
+        if B_full is None:
+            return
+        if not self.cuda:
+            for c, (j0, j1) in enumerate(self.cols):
+                if self.dist:
+                    works[c].wait()
+                self._unpack_chunk(c, j0, j1, self.gathered[slot][c] if self.dist else self.local[slot][c], B_full)
+            return
+        self.xs.wait_stream(main)   # the shards (and B_full's previous users) are done
+        with torch.cuda.stream(self.xs):
+            for c, (j0, j1) in enumerate(self.cols):
+                if self.dist:
+                    works[c].wait()   # this stream waits for the collective
+                src = self.gathered[slot][c] if self.dist else self.local[slot][c]
+                self._unpack_chunk(c, j0, j1, src, B_full)
+            ev = torch.cuda.Event()
+            ev.record(self.xs)
+        self.slot_free[slot] = ev
+
+    def wait(self) -> None:
+        """Make the caller's current stream wait for every enqueued exchange (B_full complete)."""
+        if self.cuda:
+            torch.cuda.current_stream(self.xs.device).wait_stream(self.xs)
+
+    def compute_ms(self) -> Optional[float]:
+        """Mean compute milliseconds per timed step (start to compute done on the compute stream,
+        after a synchronize)."""
+        if not self.marks:
+            return None
+        return sum(a.elapsed_time(b) for a, b in self.marks) / len(self.marks)
+
+
+class RowShardedSketch(_Pipeline):
+    """Output-row shards of a dense sketch (d_total x n, ColMajor): rank g computes rows
+    [g d_loc, (g+1) d_loc) through compute(ro_s, j0, j1, out)."""
+
+    def __init__(self, d_total: int, n: int, compute: Callable[[int, int, int, torch.Tensor], None],
+                 dtype: torch.dtype, device, chunks: int = 1, group=None):
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        if d_total % world:
+            raise ValueError(f"d_total={d_total} is not divisible by the world size {world}")
         self.d_total, self.n = d_total, n
-        self.d_loc = d_total // self.world
+        self.d_loc = d_total // world
         self.compute = compute
-        self.chunks = max(1, min(chunks, n))
-        bounds = [round(i * n / self.chunks) for i in range(self.chunks + 1)]
-        self.cols = [(bounds[i], bounds[i + 1]) for i in range(self.chunks) if bounds[i + 1] > bounds[i]]
-        self.local = [torch.empty(self.d_loc * (j1 - j0), dtype=dtype, device=device) for j0, j1 in self.cols]
-        self.gathered = [torch.empty(self.world * self.d_loc * (j1 - j0), dtype=dtype, device=device)
-                         for j0, j1 in self.cols]
-        self.streams = _Streams(torch.device(device))
+        super().__init__(_column_chunks(n, chunks), lambda nc: self.d_loc * nc, dtype, device, group)
 
     @property
     def ro_s(self) -> int:
         return self.rank * self.d_loc
 
-    def __call__(self, B_full: Optional[torch.Tensor]) -> None:
-        """Compute this rank's shard; if B_full (ColMajor d_total x n, 1-D) is given, reassemble the
-        whole sketch into it on every rank."""
-        works: List = []
-        self.streams.begin()
-        for c, (j0, j1) in enumerate(self.cols):
-            with self.streams.ctx(c):   # the gather waits for this chunk's stream only
-                self.compute(self.ro_s, j0, j1, self.local[c])
-                if self.dist and B_full is not None:
-                    works.append(dist.all_gather_into_tensor(self.gathered[c], self.local[c], group=self.group,
-                                                             async_op=True))
-        self.streams.end()
-        if B_full is None:
-            return
-        for c, (j0, j1) in enumerate(self.cols):
-            nc = j1 - j0
-            # ColMajor d_total x n: column j of rank g's shard lands at j * d_total + g * d_loc
-            if self.dist:
-                works[c].wait()
-            src = self.gathered[c] if self.dist else self.local[c]
-            _unpack(src, self.world, nc, self.d_loc, B_full[j0 * self.d_total:], self.d_total, self.d_loc)
-        self.streams.done()
+    def _compute(self, c, j0, j1, out):
+        self.compute(self.ro_s, j0, j1, out)
+
+    def _unpack_chunk(self, c, j0, j1, src, B_full):
+        # ColMajor d_total x n: column j of rank g's shard lands at j * d_total + g * d_loc
+        _unpack(src, self.world, j1 - j0, self.d_loc, B_full[j0 * self.d_total:], self.d_total, self.d_loc)
 
 
-class ColumnShardedSketch:
-    """Column sharding for the SASO sketch ("SASO partitioning"): rank g owns
-    columns [g*n_loc, (g+1)*n_loc) of A and of B. A sparse operator's columns are pure functions of
-    (seed, k) (sparse_skops.hh:72-92), so every rank samples the same S locally and reads only its
-    own m x n_loc block of A -- no rank reads another's columns. B is ColMajor, so each rank's
-    shard is a contiguous d x n_loc block and the all-gather writes the reassembled sketch with
-    one strided copy per chunk. The all-gather of chunk c overlaps the compute of chunk c+1.
-
-    compute(j0, j1, out) writes the local columns j0 .. j1 (relative to this rank's block) as a
-    ColMajor d x (j1-j0) matrix into the 1-D tensor `out`."""
+class ColumnShardedSketch(_Pipeline):
+    """Column shards for the SASO sketch ("SASO partitioning"): rank g owns columns
+    [g*n_loc, (g+1)*n_loc) of A and of B. B is ColMajor, so each rank's shard is a contiguous
+    d x n_loc block and one strided copy per chunk places the gathered blocks."""
 
     def __init__(self, d: int, n_loc: int, compute: Callable[[int, int, torch.Tensor], None],
-                 dtype: torch.dtype, device: torch.device, chunks: int = 4, group=None):
-        self.group = group
-        self.dist = dist.is_initialized()
-        self.world = dist.get_world_size(group) if self.dist else 1
-        self.rank = dist.get_rank(group) if self.dist else 0
+                 dtype: torch.dtype, device, chunks: int = 1, group=None):
         self.d, self.n_loc = d, n_loc
         self.compute = compute
-        self.chunks = max(1, min(chunks, n_loc))
-        bounds = [round(i * n_loc / self.chunks) for i in range(self.chunks + 1)]
-        self.cols = [(bounds[i], bounds[i + 1]) for i in range(self.chunks) if bounds[i + 1] > bounds[i]]
-        self.local = [torch.empty(d * (j1 - j0), dtype=dtype, device=device) for j0, j1 in self.cols]
-        self.gathered = [torch.empty(self.world * d * (j1 - j0), dtype=dtype, device=device)
-                         for j0, j1 in self.cols]
-        self.streams = _Streams(torch.device(device))
+        super().__init__(_column_chunks(n_loc, chunks), lambda nc: d * nc, dtype, device, group)
 
     @property
     def co(self) -> int:
         """First global column of this rank's block."""
         return self.rank * self.n_loc
 
-    def __call__(self, B_full: Optional[torch.Tensor]) -> None:
-        """Compute this rank's columns; if B_full (ColMajor d x world*n_loc, 1-D) is given, gather the
-        whole sketch into it on every rank."""
-        works: List = []
-        self.streams.begin()
-        for c, (j0, j1) in enumerate(self.cols):
-            with self.streams.ctx(c):
-                self.compute(j0, j1, self.local[c])
-                if self.dist and B_full is not None:
-                    works.append(dist.all_gather_into_tensor(self.gathered[c], self.local[c], group=self.group,
-                                                             async_op=True))
-        self.streams.end()
-        if B_full is None:
-            return
-        for c, (j0, j1) in enumerate(self.cols):
-            nc = j1 - j0
-            # [rank][local column][row]: rank g's column j0 + j at (g n_loc + j0 + j) d
-            if self.dist:
-                works[c].wait()
-            src = self.gathered[c] if self.dist else self.local[c]
-            _unpack(src, self.world, nc, self.d, B_full[j0 * self.d:], self.d, self.n_loc * self.d)
-        self.streams.done()
+    def _compute(self, c, j0, j1, out):
+        self.compute(j0, j1, out)
+
+    def _unpack_chunk(self, c, j0, j1, src, B_full):
+        # [rank][local column][row]: rank g's column j0 + j at (g n_loc + j0 + j) d
+        _unpack(src, self.world, j1 - j0, self.d, B_full[j0 * self.d:], self.d, self.n_loc * self.d)
+
+
+def dense_rank_compute(S, A: torch.Tensor, lda: int, m: int, d_loc: int, n: int, options=None):
+    """compute(ro_s, j0, j1, out) for RowShardedSketch over the HIP library: the ColMajor left sketch
+    B[ro_s : ro_s + d_loc, j0 : j1] = S[ro_s : ro_s + d_loc, :] A[:, j0 : j1] (A ColMajor m x n with
+    leading dimension lda, on the device). Every chunk call uses the split-K factor the library
+    chooses for the rank's WHOLE d_loc x n problem (rbh_lskge3_plan), so a chunked step gives the
+    unchunked call's bits. S is a DenseSkOp; options (rb.Options) may fix the split itself."""
+    import randblas_amd as rb
+
+    tag = "f64" if A.dtype == torch.float64 else "f32"
+    split = {}
+
+    def compute(ro_s, j0, j1, out):
+        if ro_s not in split:
+            base = options or rb.Options()
+            if base.splitk:
+                split[ro_s] = base
+            else:
+                plan = rb.plan_left("C", "N", "N", d_loc, n, m, S, A, lda, d_loc, ro_s=ro_s, dtype=tag, options=base)
+                split[ro_s] = rb.Options(splitk=plan.splitk, materialise=base.materialise)
+        rb.sketch_general_left("C", "N", "N", d_loc, j1 - j0, m, 1.0, S, A[j0 * lda:], lda, 0.0, out, d_loc,
+                               ro_s=ro_s, options=split[ro_s])
+
+    return compute

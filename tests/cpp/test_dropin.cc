@@ -417,11 +417,20 @@ static void symmetric_one_triangle() {
     std::vector<double> B1(d * n), B2(d * n), B3(d * n);
     RandBLAS::sketch_general(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, n, 1.0, S, A.data(), n, 0.0, B1.data(), d);
     RandBLAS::sketch_symmetric(Layout::ColMajor, 1.0, S, A.data(), n, 0.0, B2.data(), d);
+    CHECK(rbh_sketch_symmetric_last_path() == 0);   // default: full storage
+    std::vector<double> B4(d * n);
+    {   // asked to read one triangle (per call, scoped): the upper triangle only, the same bits
+        RandBLAS::ext::ScopedOptions o({0, 0, 1, 0});
+        RandBLAS::sketch_symmetric(Layout::ColMajor, 1.0, S, A.data(), n, 0.0, B4.data(), d);
+        CHECK(rbh_sketch_symmetric_last_path() == 1);
+    }
+    CHECK(RandBLAS::ext::thread_options().sksy_triangle == 0);   // restored at scope exit
     RandBLAS::ext::sketch_symmetric_triangle(blas::Side::Left, Layout::ColMajor, blas::Uplo::Upper, true, d, n, 1.0, S,
                                              (int64_t)0, (int64_t)0, AP.data(), (int64_t)0, 0.0, B3.data(), d);
     for (int64_t e = 0; e < d * n; ++e) {
         CHECK(B2[e] == B1[e]);
         CHECK(B3[e] == B1[e]);
+        CHECK(B4[e] == B1[e]);
     }
 }
 

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert rb.abi_version() == 1
+    assert rb.abi_version() == 2
 
 
 @pytest.mark.parametrize("dims", [(10, 37), (37, 10), (64, 64), (5, 3), (1024, 16384)])
@@ -107,3 +107,55 @@ def test_header_structs_match_ctypes():
     assert ctypes.sizeof(rb.RNGStateC) == 24
     assert ctypes.sizeof(rb.DenseDistC) == 24
     assert ctypes.sizeof(rb.SparseDistC) == 32
+    assert ctypes.sizeof(rb.OptionsC) == 16
+    assert ctypes.sizeof(rb.PlanC) == 24
+
+
+# --------------------------------------------------------------------------------------------
+# Plans and per-call options (rbh_lskge3_plan: host logic only, no launch). Without a GPU the
+# library assumes MI355X's 256 compute units.
+# --------------------------------------------------------------------------------------------
+def _plan(d, n, m, D_rows=None, ro=0, dtype="f64", opts=None, layout="C"):
+    S = rb.DenseSkOp(rb.DenseDist(D_rows or d, m), rb.RNGState(0))
+    lda, ldb = (m, d) if layout == "C" else (n, n)
+    return rb.plan_left(layout, "N", "N", d, n, m, S, 256, lda, ldb, ro_s=ro, dtype=dtype, options=opts)
+
+
+def test_plan_baseline_configs():
+    # C2 (512 wide tiles) and C4 per GPU (256): full grids, no split
+    assert _plan(1024, 16384, 16384) == rb.Plan("wide", 1, 512, 512)
+    assert _plan(256, 32768, 32768, D_rows=2048, ro=1792, dtype="f32") == rb.Plan("wide32", 1, 256, 256)
+    # C1: 16 tiles -> 16 slices of K = 4096
+    assert _plan(128, 4096, 4096) == rb.Plan("wide", 16, 16, 256)
+    # the north star split over 8 ranks: 128 tiles fill half the chip -> split 2
+    assert _plan(256, 16384, 16384, D_rows=2048, ro=1792) == rb.Plan("wide", 2, 128, 256)
+    # a quarter of C4's rank columns alone would split 4: the sharded driver passes the whole split
+    assert _plan(256, 8192, 32768, D_rows=2048, ro=1792, dtype="f32") == rb.Plan("wide32", 4, 64, 256)
+    # K below 2048 never splits (every kernel then adds in the same order)
+    assert _plan(128, 4096, 1024).splitk == 1
+
+
+def test_plan_options_fix_the_split():
+    assert _plan(128, 4096, 4096, opts=rb.Options(splitk=1)).splitk == 1
+    assert _plan(128, 4096, 4096, opts=rb.Options(splitk=3)) == rb.Plan("wide", 3, 16, 48)
+    assert _plan(1024, 16384, 16384, opts=rb.Options(splitk=2)).splitk == 2
+    # RowMajor A with lda = n is contiguous along the output columns, not along the contracted
+    # index: the generic kernel (scalar loads along the outer index)
+    assert _plan(1024, 16384, 16384, layout="R").kernel == "generic"
+    # f32 with K not a multiple of 32: the fused kernel
+    assert _plan(256, 4096, 4004, dtype="f32").kernel == "fused"
+    with pytest.raises(rb.RandBLASError) as ei:
+        _plan(128, 4096, 4096, opts=rb.Options(splitk=-1))
+    assert "opt->splitk >= 0" in str(ei.value)
+
+
+def test_unpack_shards_rejects_host_pointers():
+    """rbh_unpack_shards takes device pointers only: host arrays give RBH_ERR_REQUIRE (the Python
+    wrapper refuses CPU tensors before the call)."""
+    src, dst = np.zeros(16), np.zeros(16)
+    rc = rb.lib.rbh_unpack_shards(src.ctypes.data, 2, 2, 4, dst.ctypes.data, 4, 8, 8, None)
+    assert rc == rb.RBH_ERR_REQUIRE
+    assert "rbh_is_device_pointer" in rb.lib.rbh_last_error().decode()
+    import torch
+    with pytest.raises(ValueError):
+        rb.unpack_shards(torch.zeros(16, dtype=torch.float64), 2, 2, 4, torch.zeros(16, dtype=torch.float64), 4, 8)

@@ -18,9 +18,3 @@ def test_cpp_dropin_client(tmp_path):
     out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "ALL PASSED" in out.stdout
-    # again with sketch_symmetric reading one triangle of a bitwise-symmetric A (RBH_SKSY_TRI=1):
-    # the same bits as sketch_general on all of A
-    out = subprocess.run([exe], capture_output=True, text=True, timeout=300,
-                         env=dict(os.environ, RBH_SKSY_TRI="1"))
-    assert out.returncode == 0, out.stdout + out.stderr
-    assert "ALL PASSED" in out.stdout

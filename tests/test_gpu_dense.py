@@ -84,7 +84,7 @@ def _pos(layout, lds, ro, co):
 
 
 def check_left(cuda, layout, opS, opA, d, n, m, alpha, beta, SR, SC, ro, co, dtype, fam="G", maj="L",
-               explicit=False, skey=0):
+               explicit=False, skey=0, options=None):
     rA, cA = (m, n) if opA == "N" else (n, m)
     A = O.random_matrix(rA, cA, 99, dtype)
     lda = rA if layout == "C" else cA
@@ -102,7 +102,8 @@ def check_left(cuda, layout, opS, opA, d, n, m, alpha, beta, SR, SC, ro, co, dty
         Sop.buff = dev(S, cuda)
         Sop.buff_layout = layout
     dB = dev(B0, cuda)
-    rb.sketch_general_left(layout, opS, opA, d, n, m, alpha, Sop, dev(A, cuda), lda, beta, dB, ldb, ro_s=ro, co_s=co)
+    rb.sketch_general_left(layout, opS, opA, d, n, m, alpha, Sop, dev(A, cuda), lda, beta, dB, ldb, ro_s=ro, co_s=co,
+                           options=options)
     got = host(dB)
     err = np.abs(got - Bexp)
     assert np.all(err <= E), f"max err/E = {np.max(err / np.maximum(E, np.finfo(dtype).tiny))}"
@@ -191,7 +192,7 @@ def test_lskge3_identity_probe(cuda):
 
 
 def check_right(cuda, layout, opA, opS, m, d, n, alpha, beta, SR, SC, ro, co, dtype, fam="G", maj="L",
-                explicit=False, skey=0):
+                explicit=False, skey=0, options=None):
     rA, cA = (m, n) if opA == "N" else (n, m)
     A = O.random_matrix(rA, cA, 57, dtype)
     lda = rA if layout == "C" else cA
@@ -210,7 +211,8 @@ def check_right(cuda, layout, opA, opS, m, d, n, alpha, beta, SR, SC, ro, co, dt
         Sop.buff = dev(S, cuda)
         Sop.buff_layout = layout
     dB = dev(B0, cuda)
-    rb.sketch_general_right(layout, opA, opS, m, d, n, alpha, dev(A, cuda), lda, Sop, beta, dB, ldb, ro_s=ro, co_s=co)
+    rb.sketch_general_right(layout, opA, opS, m, d, n, alpha, dev(A, cuda), lda, Sop, beta, dB, ldb, ro_s=ro, co_s=co,
+                            options=options)
     got = host(dB)
     err = np.abs(got - Bexp)
     assert np.all(err <= E), f"max err/E = {np.max(err / np.maximum(E, np.finfo(dtype).tiny))}"
@@ -267,48 +269,86 @@ def test_row_shards_reassemble(cuda):
 
 
 # Memory operands spanning >= 4 wide tiles (here 2100 outer indices): the drawing wide kernels (the
-# default: the operator tile is regenerated in LDS and never stored) and, with RBH_MATERIALISE=1, the
-# opt-in materialised-operator kernels (gen_fill_kernel + the GMAT wide kernels). Generated rows not
+# default: the operator tile is regenerated in LDS and never stored) and, with Options(materialise),
+# the opt-in materialised-operator kernels (gen_fill_kernel + the GMAT wide kernels). Generated rows not
 # a multiple of 64, a ragged last tile, a submatrix window, both families and major axes, f64 and
 # f32 (K = 256 is a multiple of both step depths), left and right sketches.
 @pytest.fixture(params=["draw", "materialise"])
-def operator_mode(request, monkeypatch):
-    if request.param == "materialise":
-        monkeypatch.setenv("RBH_MATERIALISE", "1")
-    else:
-        monkeypatch.delenv("RBH_MATERIALISE", raising=False)
-    return request.param
+def operator_mode(request):
+    return rb.Options(materialise=request.param == "materialise")
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("layout", ["C", "R"])
 @pytest.mark.parametrize("fam,maj", [("G", "L"), ("G", "S"), ("U", "L")])
 def test_lskge3_wide_tiles(cuda, operator_mode, dtype, layout, fam, maj):
-    check_left(cuda, layout, "N", "N", 100, 2100, 256, 1.5, 0.5, 120, 300, 8, 4, dtype, fam=fam, maj=maj)
+    check_left(cuda, layout, "N", "N", 100, 2100, 256, 1.5, 0.5, 120, 300, 8, 4, dtype, fam=fam, maj=maj,
+               options=operator_mode)
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("layout", ["C", "R"])
 @pytest.mark.parametrize("fam,maj", [("G", "L"), ("U", "S")])
 def test_rskge3_wide_tiles(cuda, operator_mode, dtype, layout, fam, maj):
-    check_right(cuda, layout, "N", "N", 2100, 100, 256, -0.5, 0.0, 300, 120, 4, 8, dtype, fam=fam, maj=maj)
+    check_right(cuda, layout, "N", "N", 2100, 100, 256, -0.5, 0.0, 300, 120, 4, 8, dtype, fam=fam, maj=maj,
+                options=operator_mode)
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
-def test_materialised_equals_drawn_bitwise(cuda, monkeypatch, dtype):
+def test_materialised_equals_drawn_bitwise(cuda, dtype):
     """The opt-in materialised window feeds the wide kernel the same LDS image in the same MFMA
     order as the in-kernel draw: bitwise the same sketch."""
     d, n, m = 130, 2600, 512
     A = dev(O.random_matrix(m, n, 99, dtype), cuda)
     S = rb.DenseSkOp(rb.DenseDist(d + 6, m + 32), rb.RNGState(3))
     out = []
-    for mode in ("0", "1"):
-        monkeypatch.setenv("RBH_MATERIALISE", mode)
+    for mat in (False, True):
         B = torch.empty(d * n, dtype=A.dtype, device=cuda)
-        rb.sketch_general_left("C", "N", "N", d, n, m, dtype(1.0), S, A, m, dtype(0.0), B, d, ro_s=4, co_s=8)
+        rb.sketch_general_left("C", "N", "N", d, n, m, dtype(1.0), S, A, m, dtype(0.0), B, d, ro_s=4, co_s=8,
+                               options=rb.Options(materialise=mat))
         out.append(host(B))
     ut = np.uint64 if dtype == np.float64 else np.uint32
     assert np.array_equal(out[0].view(ut), out[1].view(ut))
+
+
+# Split-K on the wide kernels (What the multi-GPU dense runs execute: a rank's column chunk of
+# BASELINE configs[3] has 64 wide tiles and runs the f32 32-deep kernel split 4). d = 128, m = n =
+# 4096: 16 output tiles at K = 4096 -> automatic split 16; forced 1 (unsplit) and 3 (uneven
+# slices). RowMajor with opA = T keeps A contiguous along the contracted index (the wide kernels'
+# memory operand). Within E of the oracle; the plan names the kernel that ran.
+@pytest.mark.parametrize("dtype,kernel", [(np.float32, "wide32"), (np.float64, "wide")])
+@pytest.mark.parametrize("layout,opA", [("C", "N"), ("R", "T")])
+@pytest.mark.parametrize("split", [0, 1, 3])
+def test_wide_split_k_within_bound(cuda, dtype, kernel, layout, opA, split):
+    d, n, m = 128, 4096, 4096
+    opts = rb.Options(splitk=split)
+    S = rb.DenseSkOp(rb.DenseDist(d + 4, m), rb.RNGState(0))
+    lda = m
+    plan = rb.plan_left(layout, "N", opA, d, n, m, S, 256, lda, d if layout == "C" else n, ro_s=4,
+                        dtype="f64" if dtype == np.float64 else "f32", options=opts)
+    assert plan.kernel == kernel and plan.splitk == (16 if split == 0 else split), plan
+    check_left(cuda, layout, "N", opA, d, n, m, 1.0, -0.5, d + 4, m, 4, 0, dtype, options=opts)
+
+
+def test_f32_split_chunks_bitwise_with_whole_split(cuda):
+    """Column chunks computed with the whole problem's split (what RowShardedSketch's
+    dense_rank_compute does: 32 tiles -> split 8) give the unchunked call's bits, although a
+    chunk of 1024 columns alone (8 tiles) would split 32."""
+    from randblas_amd.distributed import dense_rank_compute
+
+    d, m, n = 256, 8192, 4096
+    A = dev(O.random_matrix(m, n, 99, np.float32), cuda)
+    S = rb.DenseSkOp(rb.DenseDist(2048, m), rb.RNGState(0))
+    ref = torch.empty(d * n, dtype=torch.float32, device=cuda)
+    rb.sketch_general_left("C", "N", "N", d, n, m, 1.0, S, A, m, 0.0, ref, d, ro_s=1792)
+    whole = rb.plan_left("C", "N", "N", d, n, m, S, A, m, d, ro_s=1792, dtype="f32")
+    assert whole.kernel == "wide32" and whole.splitk == 8, whole   # 32 tiles -> 256 / 32
+    comp = dense_rank_compute(S, A, m, m, d, n)
+    B = torch.empty_like(ref)
+    for j0, j1 in ((0, 1024), (1024, 2048), (2048, 3072), (3072, 4096)):
+        comp(1792, j0, j1, B[j0 * d:j1 * d])
+    got, exp = host(B), host(ref)
+    assert np.array_equal(got.view(np.uint32), exp.view(np.uint32))
 
 
 def test_release_workspaces(cuda):

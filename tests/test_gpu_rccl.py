@@ -29,10 +29,14 @@ def _torchrun(args, timeout=110):
 
 
 @pytest.mark.gpu
-def test_sharded_drivers_over_rccl_bitwise():
-    r = _torchrun([os.path.join("tests", "rccl_worker.py")])
+@pytest.mark.parametrize("mode", ["small", "c4", "ns"])
+def test_sharded_drivers_over_rccl_bitwise(mode):
+    """tests/rccl_worker.py: the sharded drivers over an RCCL group of one; 'c4' and 'ns' run the
+    per-rank problems of the 8-GPU dense runs (BASELINE configs[3]; the north star split over 8)
+    with 4 column chunks, bitwise against the unchunked call and within E of the oracle."""
+    r = _torchrun([os.path.join("tests", "rccl_worker.py"), mode])
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
-    assert "rccl_worker: ok" in r.stdout
+    assert f"rccl_worker {mode}: ok" in r.stdout
 
 
 @pytest.mark.gpu

@@ -67,7 +67,11 @@ def test_row_sharded_driver_world1(cuda):
     def compute(ro, j0, j1, out):
         rb.sketch_general_left("C", "N", "N", d, j1 - j0, m, 1.0, S, A[j0 * m:], m, 0.0, out, d, ro_s=ro)
 
-    B = torch.empty(d * n, dtype=torch.float64, device=cuda)
-    RowShardedSketch(d, n, compute, torch.float64, cuda, chunks=3)(B)
-    torch.cuda.synchronize()
-    assert torch.equal(B, ref)
+    for chunks in (1, 3):
+        B = torch.empty(d * n, dtype=torch.float64, device=cuda)
+        drv = RowShardedSketch(d, n, compute, torch.float64, cuda, chunks=chunks)
+        for _ in range(3):   # pipelined steps: the two buffer slots are reused
+            drv(B)
+        drv.wait()
+        torch.cuda.synchronize()
+        assert torch.equal(B, ref)

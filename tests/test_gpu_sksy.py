@@ -161,19 +161,34 @@ def full_sketch(cuda, side, layout, d, n, M, dtype=np.float64, major="L", key=5,
 @pytest.mark.parametrize("side", ["L", "R"])
 @pytest.mark.parametrize("layout", ["C", "R"])
 @pytest.mark.parametrize("n", [700, 1040])
-def test_sketch_symmetric_reads_one_triangle_bitwise(cuda, side, layout, n):
+@pytest.mark.parametrize("triangle", [False, True])
+def test_sketch_symmetric_storage_paths_bitwise(cuda, side, layout, n, triangle):
+    """sketch_symmetric on a bitwise-symmetric A: by default it reads A's full storage; asked per call
+    (Options(sksy_triangle=True)) it reads only the upper triangle -- the lower one then holds NaN,
+    which full storage would carry into the result. Both give the full-storage product's bits, and
+    rbh_sketch_symmetric_last_path reports which storage was read."""
     d = 96
     M = sym_full(n, 3)
     ref, S, ldb = full_sketch(cuda, side, layout, d, n, M)
     br, bc = (d, n) if side == "L" else (n, d)
     B = torch.zeros(br * bc, dtype=torch.float64, device=cuda)
     A = dev(store(M, layout, n), cuda)
+    opts = rb.Options(sksy_triangle=triangle)
     if side == "L":
-        rb.sketch_symmetric_left(layout, d, n, 0.75, S, A, n, 0.0, B, ldb, ro_s=2, co_s=4)
+        rb.sketch_symmetric_left(layout, d, n, 0.75, S, A, n, 0.0, B, ldb, ro_s=2, co_s=4, options=opts)
     else:
-        rb.sketch_symmetric_right(layout, n, d, 0.75, A, n, S, 0.0, B, ldb, ro_s=2, co_s=4)
+        rb.sketch_symmetric_right(layout, n, d, 0.75, A, n, S, 0.0, B, ldb, ro_s=2, co_s=4, options=opts)
+    assert rb.sketch_symmetric_last_path() == ("upper" if triangle else "full")
     got = host(B)
     assert np.array_equal(got.view(np.uint64), ref.view(np.uint64)), f"{np.sum(got != ref)} differ"
+    if triangle:   # the lower triangle is never read: poison it after the check, and sketch again
+        Ap = dev(poison_other_triangle(store(M, layout, n), n, n, layout, "U"), cuda)
+        B2 = torch.zeros_like(B)
+        # (sketch_symmetric's check reads both triangles, so a poisoned A fails it: the one-triangle
+        # kernel its triangle path runs is driven directly here)
+        rb.sketch_symmetric_tri(layout, side, "U", "F", d, n, 0.75, S, Ap, n, 0.0, B2, ldb, ro_s=2, co_s=4)
+        got2 = host(B2)
+        assert np.array_equal(got2.view(np.uint64), ref.view(np.uint64))
 
 
 def test_sketch_symmetric_triangle_vs_oracle(cuda):
@@ -196,15 +211,11 @@ def test_sketch_symmetric_triangle_vs_oracle(cuda):
 @pytest.mark.parametrize("uplo", ["U", "L"])
 @pytest.mark.parametrize("fmt", ["F", "P"])
 @pytest.mark.parametrize("n,mat", [(600, False), (2560, False), (2560, True)])
-def test_sksy_tri_full_and_packed(cuda, side, layout, uplo, fmt, n, mat, monkeypatch):
+def test_sksy_tri_full_and_packed(cuda, side, layout, uplo, fmt, n, mat):
     """rbh_sksy_tri: only triangle uplo is read (the other holds NaN), beta != 0, full or packed.
     n = 2560 spans five 512-row memory tiles (every tile class of the one-triangle kernel: inside
     the triangle, mirrored and straddling the diagonal, several times per output tile); with mat
-    the operator window is materialised first (RBH_MATERIALISE=1, the kernels' GMAT form)."""
-    if mat:
-        monkeypatch.setenv("RBH_MATERIALISE", "1")
-    else:
-        monkeypatch.delenv("RBH_MATERIALISE", raising=False)
+    the operator window is materialised first (Options(materialise), the kernels' GMAT form)."""
     d = 80
     M = sym_full(n, 6)
     br, bc = (d, n) if side == "L" else (n, d)
@@ -217,7 +228,8 @@ def test_sksy_tri_full_and_packed(cuda, side, layout, uplo, fmt, n, mat, monkeyp
     else:
         lda, A = 0, packed(M, layout, uplo)
     B = dev(B0, cuda)
-    rb.sketch_symmetric_tri(layout, side, uplo, fmt, d, n, 0.75, S, dev(A, cuda), lda, -0.5, B, ldb, ro_s=2, co_s=4)
+    rb.sketch_symmetric_tri(layout, side, uplo, fmt, d, n, 0.75, S, dev(A, cuda), lda, -0.5, B, ldb, ro_s=2, co_s=4,
+                            options=rb.Options(materialise=mat))
     got = host(B)
     assert np.array_equal(got.view(np.uint64), ref.view(np.uint64)), f"{np.sum(got != ref)} differ"
 

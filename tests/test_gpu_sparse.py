@@ -218,3 +218,92 @@ def test_index_mode_repeated(cuda, dtype, layout, given):
         rb.sketch_general_left(layout, "N", "N", d, n, m, 1.0, S, dA, lda, 0.0, dB, ldb)
         got = host(dB)
         assert np.array_equal(bits(got), bits(Bexp)), f"repetition {rep}: {np.count_nonzero(bits(got) != bits(Bexp))} differ"
+
+
+# --------------------------------------------------------------------------------------------
+# Filled operators (the reference's fill-once / apply-many use: skge.hh:503-504 applies an operator
+# that is known_filled from its arrays; sparse_skops.hh:389-413 fills it; examples/total-least-
+# squares/tls_sparse_skop.cc:158): arrays whose in-window values are +-1 after alpha, without
+# repeated (row, k), take the LDS-DMA apply; the library checks that on the device.
+# --------------------------------------------------------------------------------------------
+def _oracle_left(d, n, m, alpha, rows, cols, vals, A, beta, B0, layout="C"):
+    Bexp = B0.copy()
+    O.left_spmm_coo(layout, "N", "N", d, n, m, alpha, d, m, rows, cols, vals, 0, 0, A, m, beta, Bexp, d)
+    return Bexp
+
+
+@pytest.mark.parametrize("d,m,n,vec", [(1024, 16384, 256, 8), (200, 999, 130, 3), (40, 100, 16, 2)])
+@pytest.mark.parametrize("alpha", [1.0, -1.0])
+def test_fill_sparse_op_applies_on_dma_path(cuda, d, m, n, vec, alpha):
+    """fill_sparse_op(S) once, then two sketches from its arrays (sparse_filled: no host wait):
+    the LDS-DMA apply, bitwise the oracle's; the same arrays passed as a plain user operator (origin
+    unknown: the call waits for the device check) give the same bits on the same path."""
+    A = O.random_matrix(m, n, 99)
+    B0 = O.random_matrix(d, n, 42)
+    rows, cols, vals = O.fill_sparse(d, m, vec, "S", key=3)
+    Bexp = _oracle_left(d, n, m, alpha, rows, cols, vals, A, 0.5, B0)
+    S = rb.fill_sparse_op(rb.SparseSkOp(rb.SparseDist(d, m, vec), rb.RNGState(3)))
+    assert np.array_equal(host(S.rows), rows) and np.array_equal(host(S.vals), vals)
+    dA = dev(A, cuda)
+    for _ in range(2):
+        dB = dev(B0, cuda)
+        rb.sketch_general_left("C", "N", "N", d, n, m, alpha, S, dA, m, 0.5, dB, d)
+        assert rb.sparse_last_path() == "dma"
+        got = host(dB)
+        assert np.array_equal(bits(got), bits(Bexp)), f"{np.sum(got != Bexp)} differ"
+    U = rb.SparseSkOp(rb.SparseDist(d, m, vec), rb.RNGState(3), S.rows, S.cols, S.vals, S.nnz)
+    dB = dev(B0, cuda)
+    rb.sketch_general_left("C", "N", "N", d, n, m, alpha, U, dA, m, 0.5, dB, d)
+    assert rb.sparse_last_path() == "dma"
+    assert np.array_equal(bits(host(dB)), bits(Bexp))
+
+
+def test_user_arrays_scaled_values_take_dma_path(cuda):
+    """Values +-2 applied with alpha = 0.5: every alpha * v is +-1 exactly, so the device check
+    passes and the LDS-DMA apply gives the reference's (alpha v) * y = +-y bits."""
+    d, m, n = 300, 1000, 70
+    A = O.random_matrix(m, n, 99)
+    rows, cols, vals = O.fill_sparse(d, m, 4, "S", key=9)
+    vals = 2.0 * vals
+    Bexp = _oracle_left(d, n, m, 0.5, rows, cols, vals, A, 0.0, np.zeros(d * n))
+    S = rb.SparseSkOp(rb.SparseDist(d, m, 4), rb.RNGState(9), dev(rows, cuda), dev(cols, cuda), dev(vals, cuda))
+    dB = torch.zeros(d * n, dtype=torch.float64, device=cuda)
+    rb.sketch_general_left("C", "N", "N", d, n, m, 0.5, S, dev(A, cuda), m, 0.0, dB, d)
+    assert rb.sparse_last_path() == "dma"
+    assert np.array_equal(bits(host(dB)), bits(Bexp))
+
+
+@pytest.mark.parametrize("defect", ["value", "duplicate"])
+def test_user_arrays_failing_the_check_fall_back(cuda, defect):
+    """A value that is not +-1, or a repeated (row, k): the device check fails, the call falls back to
+    the sorted apply (duplicates are added in input order there) and stays bitwise the oracle's."""
+    d, m, n = 256, 2048, 66
+    A = O.random_matrix(m, n, 99)
+    rows, cols, vals = O.fill_sparse(d, m, 8, "S", key=4)
+    if defect == "value":
+        vals = vals.copy()
+        vals[777] = 0.25
+    else:   # entry 10 repeated (same row and column) at the end
+        rows, cols, vals = np.append(rows, rows[10]), np.append(cols, cols[10]), np.append(vals, vals[10])
+    Bexp = _oracle_left(d, n, m, 1.0, rows, cols, vals, A, 0.0, np.zeros(d * n))
+    S = rb.SparseSkOp(rb.SparseDist(d, m, 8), rb.RNGState(4), dev(rows, cuda), dev(cols, cuda), dev(vals, cuda),
+                      len(rows))
+    dB = torch.zeros(d * n, dtype=torch.float64, device=cuda)
+    rb.sketch_general_left("C", "N", "N", d, n, m, 1.0, S, dev(A, cuda), m, 0.0, dB, d)
+    assert rb.sparse_last_path() in ("sorted_unit", "sorted")
+    assert np.array_equal(bits(host(dB)), bits(Bexp))
+
+
+def test_sparse_filled_claim_that_fails_the_check_gives_nan(cuda):
+    """Options(sparse_filled=True) on arrays that are not fill_sparse's output: the apply does not wait
+    for the device check, and its failure makes the sketch NaN (loud, not silently wrong)."""
+    d, m, n = 128, 512, 64
+    rows, cols, vals = O.fill_sparse(d, m, 4, "S", key=5)
+    vals = vals.copy()
+    vals[3] = 3.0
+    S = rb.SparseSkOp(rb.SparseDist(d, m, 4), rb.RNGState(5), dev(rows, cuda), dev(cols, cuda), dev(vals, cuda))
+    dB = torch.zeros(d * n, dtype=torch.float64, device=cuda)
+    rb.sketch_general_left("C", "N", "N", d, n, m, 1.0, S, dev(O.random_matrix(m, n, 99), cuda), m, 0.0, dB, d,
+                           options=rb.Options(sparse_filled=True))
+    assert rb.sparse_last_path() == "dma"
+    assert bool(torch.isnan(dB).all())
