@@ -1148,6 +1148,246 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Streamed wide kernel (round 4): 32 generated x 1024 memory outer indices, the memory operand
+// loaded straight into MFMA fragments, the generated tile through an LDS ring
+// ------------------------------------------------------------------------------------------
+// The same sums, in the same order, as skge_wide_kernel (f64) / skge_wide32_kernel (f32): a step
+// covers 128 bytes of K per row (16 f64 / 32 f32 values), lane (g, r) of a 16 x 16 MFMA tile
+// contracts k = VPL g + v in sub-step v (VPL = 4 / 8 values), the sub-steps in ascending v, the
+// steps in ascending k; each output element's MFMA chain is therefore bit for bit the older
+// kernels' (and the one-triangle / materialised kernels', which keep the 64 x 512 tiles).
+// What changes is the data movement:
+//  * Operator draws. The generated tile is 32 rows instead of 64, for the same 1024 x 32 = 64 x 512
+//    accumulator budget, so every operator entry is drawn once per 1024 memory rows instead of per
+//    512: half the Philox + Box-Muller VALU per MFMA (on gfx950 f64 / f32 MFMAs hold their SIMD's
+//    issue, so every VALU instruction adds to the step; tools/micro/mfma_coexec.hip).
+//  * No memory tile in LDS. Wave w owns memory rows [128 w, 128 w + 128) of the tile and loads each
+//    lane's 32 B per 16-row block (two 16-B buffer loads) straight into the registers the MFMAs
+//    read: no LDS staging writes, no fragment reads, no barrier for the memory operand. Block c of
+//    step kt + 1 is loaded PF blocks ahead of its use (a ring of PF + 1 register slots).
+//  * One barrier per round of R = 4 steps. The 32 x 128-B generated tiles of a round sit in an LDS
+//    ring (2 rounds x 4 slots, 32 KiB); every wave draws its share of the NEXT round's tiles (f64:
+//    one Philox call per lane and round, f32: two) in the middle of the round, so the draw is
+//    spread evenly over the four SIMDs and the waves meet once per round.
+// Requires K % (128 / sizeof(T)) == 0, a memory operand with 16-B aligned rows contiguous along k
+// (mode 2), pc0 % 4 == 0, and the wave's 128 rows addressable with 32-bit byte offsets.
+template <typename T, int GK, int FAMILY, bool GX, bool SPLIT, int PF>
+__global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
+    constexpr int KS = 128 / (int)sizeof(T);              // k per step
+    constexpr int VPL = 32 / (int)sizeof(T);              // k values per lane and step: k = VPL g + v
+    constexpr int EPS = 16 / (int)sizeof(T);              // elements per 16-B slot
+    constexpr int BG = 32, BMW = 128;                     // generated rows; memory rows per wave
+    constexpr int FA = BG / 16, FB = BMW / 16;            // 2 x 8 MFMA tiles per wave
+    constexpr int R = 4;                                  // steps per round
+    constexpr int SLOT_B = BG * 128;                      // bytes per generated tile (32 rows x 128 B)
+    constexpr int CPS = BG * KS / 4;                      // Philox calls per step (f64 128, f32 256)
+    constexpr int WCALLS = R * CPS / 512;                 // wave-calls per wave and round (1, 2)
+    constexpr int NSLOT = PF + 1;                         // register slots of the memory prefetch ring
+    static_assert(FB % NSLOT == 0, "a block's slot must not depend on the step");
+    typedef typename Mfma<T>::v4 acc_t;
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    typedef T tv_t __attribute__((ext_vector_type(VPL)));   // a lane's VPL values of one row
+
+    __shared__ __attribute__((aligned(16))) char gring[2 * R * SLOT_B];
+    __shared__ rb::LogfEntry tab[16];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, r = lane & 15;
+    if (tid < 16) tab[tid] = rb::LOGF_TAB[tid];
+
+    const GenOperand &gop = GX ? p.xg : p.yg;
+    const MemOperand &mop = GX ? p.ym : p.xm;
+    const int64_t gnO = GX ? p.M : p.N, mnO = GX ? p.N : p.M;
+    const int64_t nTg = (gnO + BG - 1) / BG, nTm = (mnO + 8 * BMW - 1) / (8 * BMW);
+    const int split = SPLIT ? p.splitk : 1;
+    const int64_t nb = nTg * nTm * split;
+    const int64_t b = blockIdx.x;
+    const int64_t xcd = b % 8, qq = nb / 8, rr = nb % 8;
+    const int64_t t_all = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + b / 8;
+    const int64_t z = t_all % split, t = t_all / split;
+    // consecutive tiles share a memory tile (the generated tiles of one memory tile run on one XCD)
+    const int64_t go0 = (t % nTg) * BG, mo0 = (t / nTg) * (8 * BMW);
+    const int64_t wm0 = mo0 + (int64_t)wave * BMW;        // this wave's first memory row
+
+    // ---- memory operand: lane (g, r) of block c reads row wm0 + 16 c + r, bytes [32 g, 32 g + 32) of
+    // the step's 128-B window, through a buffer resource based at the wave's first row (rows past
+    // the operand clamped to its last row; their outputs are discarded)
+    const T *mptr = (const T *)mop.ptr;
+    const int64_t wbase = wm0 < mnO ? wm0 : mnO - 1;
+    const __amdgpu_buffer_rsrc_t mrsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(mptr + wbase * mop.so), (short)0, -1, 0x00020000);
+    uint32_t voff[FB];
+#pragma unroll
+    for (int c = 0; c < FB; ++c) {
+        int64_t row = wm0 + 16 * c + r;
+        row = row < mnO ? row : mnO - 1;
+        voff[c] = (uint32_t)(((row - wbase) * mop.so + (int64_t)VPL * g) * (int64_t)sizeof(T));
+    }
+    tv_t mv[NSLOT];
+    auto mload = [&](int slot, int c, int64_t kt) {
+        const uint32_t soff = (uint32_t)(kt * 128);
+        const v4f lo = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(mrsrc, voff[c], soff, 0));
+        const v4f hi = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(mrsrc, voff[c] + 16u, soff, 0));
+        typedef float v8f __attribute__((ext_vector_type(8)));
+        v8f both;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { both[e] = lo[e]; both[4 + e] = hi[e]; }
+        mv[slot] = __builtin_bit_cast(tv_t, both);
+    };
+
+    // ---- generated operand: slot (ring half, step t) holds rows o < 32 of 8 16-B slots each, slot q
+    // of row o at q ^ sw32(o) (conflict-free ds_read_b128 fragment reads, as in skge_wide32_kernel)
+    auto gslot = [&](int half, int ts) -> char * { return gring + (half * R + ts) * SLOT_B; };
+    // this lane's Philox calls of a round: call u covers step ts_u, call cc_u of that step
+    uint32_t cbase[WCALLS][4];
+    int ts_of[WCALLS], cc_of[WCALLS];
+#pragma unroll
+    for (int u = 0; u < WCALLS; ++u) {
+        const int c = 64 * wave + lane + 512 * u;
+        ts_of[u] = c / CPS;
+        cc_of[u] = c % CPS;
+        uint64_t off;
+        if (GK == GEN_OK) {   // call = (row o, k quad qd)
+            const int o = cc_of[u] / (KS / 4), qd = cc_of[u] % (KS / 4);
+            off = (uint64_t)(gop.pr0 + go0 + o) * gop.stride + (uint64_t)(gop.pc0 >> 2) + (uint64_t)ts_of[u] * (KS / 4) + qd;
+        } else {              // call = (k, row quad qo)
+            const int k = cc_of[u] / (BG / 4), qo = cc_of[u] % (BG / 4);
+            off = (uint64_t)(gop.pr0 + (int64_t)ts_of[u] * KS + k) * gop.stride + (uint64_t)((gop.pc0 + go0) >> 2) + qo;
+        }
+        rb::ctr_add(gop.ctr, off, cbase[u]);
+    }
+    // counter advance per step: GEN_OK KS / 4 quads, GEN_OO KS natural rows
+    const uint64_t cstep = GK == GEN_OK ? (uint64_t)(KS / 4) : (uint64_t)KS * gop.stride;
+    const bool gtile_full = go0 + BG <= gnO;
+    // draw call u of the round starting at step kr0 into ring half `half` (steps >= kend: nothing)
+    auto draw = [&](int u, int64_t kr0, int half, int64_t kend) {
+        const int64_t kt = kr0 + ts_of[u];
+        if (kt >= kend) return;   // (uniform per wave: ts_of is per wave for CPS >= 64)
+        uint32_t cc[4];
+        rb::ctr_add(cbase[u], (uint64_t)kr0 * cstep, cc);
+        const rb::u32x4 w = rb::philox4x32_uk<10>(cc[0], cc[1], cc[2], cc[3], gop.key[0], gop.key[1]);
+        float sm[4];
+        rb::sample4<FAMILY>(w, sm, tab);
+        T v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = FAMILY == rb::UNIFORM ? (T)sm[e] * (T)gop.scale : (T)sm[e];
+        char *G = gslot(half, ts_of[u]);
+        if (GK == GEN_OK) {
+            const int o = cc_of[u] / (KS / 4), qd = cc_of[u] % (KS / 4);
+            if (!gtile_full && go0 + o >= gnO) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = (T)0;
+            }
+            // k = 4 qd .. 4 qd + 3: f32 one 16-B slot (qd), f64 two (2 qd, 2 qd + 1)
+#pragma unroll
+            for (int hsl = 0; hsl < 4 / EPS; ++hsl) {
+                const int q = qd * (4 / EPS) + hsl;
+                T *dst = (T *)(G + o * 128 + 16 * (q ^ sw32(o)));
+#pragma unroll
+                for (int e = 0; e < EPS; ++e) dst[e] = v[hsl * EPS + e];
+            }
+        } else {
+            const int k = cc_of[u] / (BG / 4), qo = cc_of[u] % (BG / 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int o = 4 * qo + e;
+                const T x = (gtile_full || go0 + o < gnO) ? v[e] : (T)0;
+                *(T *)(G + o * 128 + 16 * ((k / EPS) ^ sw32(o)) + (int)sizeof(T) * (k % EPS)) = x;
+            }
+        }
+    };
+    // a lane's generated fragment of row 16 a + r for the step in slot (half, ts): slots 2 g, 2 g + 1
+    auto gread = [&](int half, int ts, int a) -> tv_t {
+        const char *G = gslot(half, ts) + (16 * a + r) * 128;
+        const v4f lo = *reinterpret_cast<const v4f *>(G + 16 * ((2 * g) ^ sw32(r)));
+        const v4f hi = *reinterpret_cast<const v4f *>(G + 16 * ((2 * g + 1) ^ sw32(r)));
+        typedef float v8f __attribute__((ext_vector_type(8)));
+        v8f both;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { both[e] = lo[e]; both[4 + e] = hi[e]; }
+        return __builtin_bit_cast(tv_t, both);
+    };
+
+    acc_t acc[FA][FB];
+#pragma unroll
+    for (int a = 0; a < FA; ++a)
+#pragma unroll
+        for (int c = 0; c < FB; ++c) acc[a][c] = (acc_t){0, 0, 0, 0};
+
+    const int64_t nk = p.K / KS;
+    const int64_t per = SPLIT ? (nk + split - 1) / split : nk;
+    const int64_t kt0 = SPLIT ? z * per : 0, kt1 = SPLIT ? (kt0 + per < nk ? kt0 + per : nk) : nk;
+    __syncthreads();   // tab
+    // prologue: round 0's generated tiles, the first PF blocks of step kt0
+#pragma unroll
+    for (int u = 0; u < WCALLS; ++u) draw(u, kt0, 0, kt1);
+    if (kt0 < kt1) {
+#pragma unroll
+        for (int c = 0; c < PF; ++c) mload(c % NSLOT, c, kt0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+    const int64_t nrounds = (kt1 - kt0 + R - 1) / R;
+    for (int64_t rd = 0; rd < nrounds; ++rd) {
+        const int half = (int)(rd & 1);
+        const int64_t kr0 = kt0 + rd * R;
+#pragma unroll
+        for (int ts = 0; ts < R; ++ts) {
+            const int64_t kt = kr0 + ts;
+            if (kt >= kt1) break;
+            tv_t gf[FA];
+#pragma unroll
+            for (int a = 0; a < FA; ++a) gf[a] = gread(half, ts, a);
+#pragma unroll
+            for (int c = 0; c < FB; ++c) {
+                // block c + PF (this step's, or the next step's first blocks), PF blocks ahead
+                const int cn = c + PF;
+                const int64_t ktn = cn < FB ? kt : (kt + 1 < kt1 ? kt + 1 : kt);
+                mload(cn % NSLOT, cn % FB, ktn);
+                const tv_t &m = mv[c % NSLOT];
+#pragma unroll
+                for (int v = 0; v < VPL; ++v)
+#pragma unroll
+                    for (int a = 0; a < FA; ++a)
+                        acc[a][c] = GX ? Mfma<T>::mma(m[v], gf[a][v], acc[a][c]) : Mfma<T>::mma(gf[a][v], m[v], acc[a][c]);
+            }
+            // the next round's generated tiles: every wave's share, spread over the round (f64: its
+            // one call after step 1; f32: after steps 0 and 2)
+            if (rd + 1 < nrounds) {
+#pragma unroll
+                for (int u = 0; u < WCALLS; ++u)
+                    if (ts == (u * R) / WCALLS + (WCALLS == 1 ? 1 : 0)) draw(u, kr0 + R, half ^ 1, kt1);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+
+    // split-K: alpha times this split's partial sum to partial[z]; the reduction adds them in order
+    T *C = SPLIT ? (T *)p.partial + z * p.M * p.N : (T *)p.C;
+    const int64_t ldc = SPLIT ? p.M : p.ldc;
+    const T alpha = (T)p.alpha, beta = SPLIT ? (T)0 : (T)p.beta;
+#pragma unroll
+    for (int a = 0; a < FA; ++a)
+#pragma unroll
+    for (int c = 0; c < FB; ++c) {
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+            const int dr = Mfma<T>::drow(lane, reg);
+            const int64_t gi = go0 + 16 * a, mi = wm0 + 16 * c;
+            const int64_t i = GX ? gi + r : mi + r;
+            const int64_t j = GX ? mi + dr : gi + dr;
+            if (i < p.M && j < p.N) {
+                T *dst = C + i + j * ldc;
+                const T v = alpha * acc[a][c][reg];
+                *dst = (beta == (T)0) ? v : v + beta * *dst;
+            }
+        }
+    }
+}
+
 // split-K: C = sum_z partial[z] + beta C (partials already carry alpha), in a fixed order
 template <typename T>
 __global__ void splitk_reduce_kernel(int64_t M, int64_t N, int split, const T *partial, T beta, T *C, int64_t ldc) {
@@ -1446,6 +1686,53 @@ static bool wide32_ok(const GemmProblem &p) {
     return sizeof(T) == 4 && fused_ok(p) && p.K % KB32 == 0 && wide_offsets_ok<T>(p);
 }
 
+// The streamed wide kernel takes every wide-kernel problem whose operator is drawn in the GEMM (a
+// materialised window keeps the 64 x 512 GMAT kernels): same conditions, bitwise the same sums.
+template <typename T>
+static bool stream_ok(const GemmProblem &p) {
+    return !p.materialise && (sizeof(T) == 8 ? wide_ok<T>(p) : wide32_ok<T>(p));
+}
+
+constexpr int STREAM_PF = 3;   // memory blocks loaded ahead of their use (register ring of 4)
+
+template <typename T, int GK, int FAMILY, bool GX>
+static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
+    const int64_t gnO = GX ? p.M : p.N, mnO = GX ? p.N : p.M;
+    const int64_t nb = ((gnO + 31) / 32) * ((mnO + 1023) / 1024);
+    if (nb <= 0) return hipSuccess;
+    // the split of the 64 x 512 kernels (their tile count, 16-deep steps), so a materialised
+    // window, which runs them, gives the same bits
+    const int64_t nb_wide = ((gnO + 63) / 64) * ((mnO + 511) / 512);
+    const int split = choose_split(nb_wide, p.K / BK, p.split_req);
+    GemmProblem q = p;
+    q.splitk = split;
+    q.partial = nullptr;
+    hipError_t e;
+    if (split > 1) {
+        e = ws_alloc(&q.partial, sizeof(T) * (size_t)split * p.M * p.N, s);
+        if (e != hipSuccess) return e;
+    }
+    timing_begin(s);
+    if (split > 1)
+        hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, STREAM_PF>), dim3((unsigned)(nb * split)),
+                           dim3(512), 0, s, q);
+    else
+        hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, STREAM_PF>), dim3((unsigned)nb), dim3(512), 0,
+                           s, q);
+    e = hipGetLastError();
+    if (split > 1 && e == hipSuccess) {
+        hipLaunchKernelGGL(splitk_reduce_kernel<T>, dim3(2048), dim3(256), 0, s, p.M, p.N, split,
+                           (const T *)q.partial, (T)p.beta, (T *)p.C, p.ldc);
+        e = hipGetLastError();
+    }
+    timing_end(s);
+    if (split > 1) {
+        const hipError_t e2 = ws_free(q.partial, s);
+        if (e == hipSuccess) e = e2;
+    }
+    return e;
+}
+
 // the wide kernel instantiated for one-triangle operand p.tri (1-4)
 template <int FAM, bool GX>
 static hipError_t launch_wide_tri(const GemmProblem &p, hipStream_t s) {
@@ -1515,6 +1802,12 @@ static GemmPlan plan_gemm(const GemmProblem &p) {
         pl.kernel = PLAN_WIDE_TRI;
         pl.tiles = wide_tiles();
         pl.splitk = choose_split(pl.tiles, p.K / BK, p.split_req);
+    } else if (stream_ok<T>(p)) {
+        const bool gx = p.xkind != MEM;
+        const int64_t gnO = gx ? p.M : p.N, mnO = gx ? p.N : p.M;
+        pl.kernel = PLAN_STREAM;
+        pl.tiles = ((gnO + 31) / 32) * ((mnO + 1023) / 1024);
+        pl.splitk = choose_split(wide_tiles(), p.K / BK, p.split_req);   // as launch_stream
     } else if (wide_ok<T>(p)) {
         pl.kernel = PLAN_WIDE;
         pl.tiles = wide_tiles();
@@ -1548,6 +1841,15 @@ static hipError_t launch_gemm(const GemmProblem &p, hipStream_t s) {
     if (p.tri) return launch_gemm_tri<T>(p, s);
     const bool unif = (p.xkind != MEM ? p.xg.family : p.yg.family) == rb::UNIFORM;
     const int kernel = plan_gemm<T>(p).kernel;
+    if (kernel == PLAN_STREAM) {
+#define RBH_STREAM_L(GK, GX)                                                                   \
+    return unif ? launch_stream<T, GK, rb::UNIFORM, GX>(p, s) : launch_stream<T, GK, rb::GAUSSIAN, GX>(p, s)
+        if (p.xkind == GEN_OK) { RBH_STREAM_L(GEN_OK, true); }
+        if (p.xkind == GEN_OO) { RBH_STREAM_L(GEN_OO, true); }
+        if (p.ykind == GEN_OK) { RBH_STREAM_L(GEN_OK, false); }
+        if (p.ykind == GEN_OO) { RBH_STREAM_L(GEN_OO, false); }
+#undef RBH_STREAM_L
+    }
     if (kernel == PLAN_WIDE) {
 #define RBH_WIDE_L(GK, GX)                                                                     \
     return unif ? launch_wide<GK, rb::UNIFORM, GX>(p, s) : launch_wide<GK, rb::GAUSSIAN, GX>(p, s)

@@ -316,7 +316,7 @@ def test_materialised_equals_drawn_bitwise(cuda, dtype):
 # 4096: 16 output tiles at K = 4096 -> automatic split 16; forced 1 (unsplit) and 3 (uneven
 # slices). RowMajor with opA = T keeps A contiguous along the contracted index (the wide kernels'
 # memory operand). Within E of the oracle; the plan names the kernel that ran.
-@pytest.mark.parametrize("dtype,kernel", [(np.float32, "wide32"), (np.float64, "wide")])
+@pytest.mark.parametrize("dtype,kernel", [(np.float32, "stream"), (np.float64, "stream")])
 @pytest.mark.parametrize("layout,opA", [("C", "N"), ("R", "T")])
 @pytest.mark.parametrize("split", [0, 1, 3])
 def test_wide_split_k_within_bound(cuda, dtype, kernel, layout, opA, split):
@@ -342,13 +342,53 @@ def test_f32_split_chunks_bitwise_with_whole_split(cuda):
     ref = torch.empty(d * n, dtype=torch.float32, device=cuda)
     rb.sketch_general_left("C", "N", "N", d, n, m, 1.0, S, A, m, 0.0, ref, d, ro_s=1792)
     whole = rb.plan_left("C", "N", "N", d, n, m, S, A, m, d, ro_s=1792, dtype="f32")
-    assert whole.kernel == "wide32" and whole.splitk == 8, whole   # 32 tiles -> 256 / 32
+    assert whole.kernel == "stream" and whole.splitk == 8, whole   # 32 tiles -> 256 / 32
     comp = dense_rank_compute(S, A, m, m, d, n)
     B = torch.empty_like(ref)
     for j0, j1 in ((0, 1024), (1024, 2048), (2048, 3072), (3072, 4096)):
         comp(1792, j0, j1, B[j0 * d:j1 * d])
     got, exp = host(B), host(ref)
     assert np.array_equal(got.view(np.uint32), exp.view(np.uint32))
+
+
+# The streamed wide kernel (32 x 1024 tiles, memory operand straight to registers) adds every output
+# element's terms in the same MFMA order as the 64 x 512 wide kernels, which the materialised-window
+# option still runs: bitwise equal across operand orientations (left/right x layouts: the generated
+# operand as X or Y), counter directions (major axis), families, ragged tiles and split-K.
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("side,layout", [("L", "C"), ("L", "R"), ("R", "C"), ("R", "R")])
+@pytest.mark.parametrize("fam,maj", [("G", "L"), ("G", "S"), ("U", "L")])
+@pytest.mark.parametrize("shape", ["ragged", "split"])
+def test_stream_kernel_equals_wide_bitwise(cuda, dtype, side, layout, fam, maj, shape):
+    d, n, m = (100, 2100, 256) if shape == "ragged" else (64, 1100, 4096)
+    tag = "f64" if dtype == np.float64 else "f32"
+    ut = np.uint64 if dtype == np.float64 else np.uint32
+    out, plans = [], []
+    for mat in (False, True):
+        opts = rb.Options(materialise=mat)
+        if side == "L":
+            S = rb.DenseSkOp(rb.DenseDist(d + 6, m + 32, fam, maj), rb.RNGState(3))
+            opA = "N" if layout == "C" else "T"    # A contiguous along the contracted index
+            A = dev(O.random_matrix(m, n, 99, dtype) if opA == "N" else O.random_matrix(n, m, 99, dtype), cuda)
+            ldb = d if layout == "C" else n
+            B = torch.full((d * n,), 7.0, dtype=A.dtype, device=cuda)
+            plans.append(rb.plan_left(layout, "N", opA, d, n, m, S, A, m, ldb, ro_s=4, co_s=8, dtype=tag, options=opts))
+            rb.sketch_general_left(layout, "N", opA, d, n, m, dtype(1.5), S, A, m, dtype(-0.5), B, ldb, ro_s=4,
+                                   co_s=8, options=opts)
+        else:   # B (n x d) = A^T (n x m) S (m x d)
+            S = rb.DenseSkOp(rb.DenseDist(m + 32, d + 6, fam, maj), rb.RNGState(3))
+            opA = "T" if layout == "C" else "N"
+            A = dev(O.random_matrix(m, n, 99, dtype) if layout == "C" else O.random_matrix(n, m, 99, dtype), cuda)
+            ldb = n if layout == "C" else d
+            B = torch.full((n * d,), 7.0, dtype=A.dtype, device=cuda)
+            plans.append(rb.plan_right(layout, opA, "N", n, d, m, A, m, S, ldb, ro_s=8, co_s=4, dtype=tag,
+                                       options=opts))
+            rb.sketch_general_right(layout, opA, "N", n, d, m, dtype(1.5), A, m, S, dtype(-0.5), B, ldb, ro_s=8,
+                                    co_s=4, options=opts)
+        out.append(host(B))
+    assert plans[0].kernel == "stream" and plans[1].kernel in ("wide", "wide32"), plans
+    assert plans[0].splitk == plans[1].splitk and (shape == "ragged" or plans[0].splitk > 1), plans
+    assert np.array_equal(out[0].view(ut), out[1].view(ut)), f"{np.sum(out[0] != out[1])} differ"
 
 
 def test_release_workspaces(cuda):
