@@ -438,9 +438,9 @@ def main():
                                        if use_dist else "single GPU")},
             "pct_of_peak": roof["frac"] * 100.0,
             # what kernel_ms and the roofline time; any other launch of the step is in ms_per_step only
-            "dominant_kernel": {"dense": "skge_wide_kernel / skge_wide32_kernel (one per chunk)",
+            "dominant_kernel": {"dense": "skge_stream_kernel (one per chunk)",
                                 "saso": "saso_dma_kernel (sampling and the CSR build: ms_per_step only)",
-                                "sksy": "skge_wide_kernel (the symmetry check, the step's other launch: "
+                                "sksy": "skge_stream_kernel (the symmetry check, the step's other launch: "
                                         "ms_per_step only)",
                                 "sksyp": "skge_wide_kernel<TRI 3>"}[kind],
             "roofline": roof,

@@ -39,7 +39,10 @@ ColumnShardedSketch's  compute(j0, j1, out)  writes the d x (j1-j0) ColMajor blo
 local columns j0 .. j1.
 
 The all-gather runs whenever a process group is initialised, a group of one included: that is how
-the one-GPU box drives RCCL together with the HIP path (tests/test_gpu_rccl.py).
+the one-GPU box drives RCCL together with the HIP path (tests/test_gpu_rccl.py). Over a gloo group
+with device tensors (several ranks sharing the one GPU of a test box, tests/test_gpu_multirank.py)
+the shards go through host memory: each rank's HIP shard is copied to the host, all-gathered by
+gloo and copied back before the HIP unpack.
 """
 from __future__ import annotations
 
@@ -88,6 +91,8 @@ class _Pipeline:
         self.gathered = [[torch.empty(self.world * shard_elems(j1 - j0), dtype=dtype, device=device)
                           for j0, j1 in cols] for _ in range(self.SLOTS)] if self.dist else None
         self.xs = torch.cuda.Stream(device) if self.cuda else None   # exchange (unpack) stream
+        # gloo with device tensors: the collective runs on host copies of the shards
+        self.host_gather = self.dist and self.cuda and dist.get_backend(group) == "gloo"
         self.slot_free: List[Optional[torch.cuda.Event]] = [None] * self.SLOTS
         self.steps = 0
         # timing (CUDA only): per step (start, compute done) on the compute stream
@@ -119,7 +124,11 @@ class _Pipeline:
         works = []
         for c, (j0, j1) in enumerate(self.cols):
             self._compute(c, j0, j1, self.local[slot][c])
-            if self.dist and B_full is not None:   # issued behind this chunk's compute
+            if self.host_gather and B_full is not None:   # synchronous, through host memory
+                out = torch.empty(self.gathered[slot][c].shape, dtype=self.local[slot][c].dtype)
+                dist.all_gather_into_tensor(out, self.local[slot][c].cpu(), group=self.group)
+                self.gathered[slot][c].copy_(out)
+            elif self.dist and B_full is not None:   # issued behind this chunk's compute
                 works.append(dist.all_gather_into_tensor(self.gathered[slot][c], self.local[slot][c],
                                                          group=self.group, async_op=True))
         if self.cuda and self.timing:
@@ -135,7 +144,7 @@ class _Pipeline:
         self.xs.wait_stream(main)   # the shards (and B_full's previous users) are done
         with torch.cuda.stream(self.xs):
             for c, (j0, j1) in enumerate(self.cols):
-                if self.dist:
+                if works:
                     works[c].wait()   # this stream waits for the collective
                 src = self.gathered[slot][c] if self.dist else self.local[slot][c]
                 self._unpack_chunk(c, j0, j1, src, B_full)
