@@ -1693,7 +1693,14 @@ static bool stream_ok(const GemmProblem &p) {
     return !p.materialise && (sizeof(T) == 8 ? wide_ok<T>(p) : wide32_ok<T>(p));
 }
 
-constexpr int STREAM_PF = 3;   // memory blocks loaded ahead of their use (register ring of 4)
+// memory blocks loaded ahead of their use (a register ring of PF + 1 blocks); f64 is register-bound
+#ifndef RBH_STREAM_PF64
+#define RBH_STREAM_PF64 3
+#endif
+#ifndef RBH_STREAM_PF32
+#define RBH_STREAM_PF32 7
+#endif
+template <typename T> constexpr int stream_pf() { return sizeof(T) == 8 ? RBH_STREAM_PF64 : RBH_STREAM_PF32; }
 
 template <typename T, int GK, int FAMILY, bool GX>
 static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
@@ -1714,10 +1721,10 @@ static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
     }
     timing_begin(s);
     if (split > 1)
-        hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, STREAM_PF>), dim3((unsigned)(nb * split)),
+        hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, stream_pf<T>()>), dim3((unsigned)(nb * split)),
                            dim3(512), 0, s, q);
     else
-        hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, STREAM_PF>), dim3((unsigned)nb), dim3(512), 0,
+        hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, stream_pf<T>()>), dim3((unsigned)nb), dim3(512), 0,
                            s, q);
     e = hipGetLastError();
     if (split > 1 && e == hipSuccess) {

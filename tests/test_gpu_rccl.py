@@ -50,4 +50,4 @@ def test_bench_dist_step_over_rccl(config):
     assert line["n_gpus"] == 1 and "RCCL all-gather" in line["config"]["parallelism"]
     assert line["value"] > 0 and line["kernel_launches_per_step"] >= 1
     assert line["compute_ms_per_step"] > 0 and line["exposed_exchange_ms_per_step"] >= 0
-    assert line["roofline"]["basis"] == "step"
+    assert line["roofline"]["basis"] == "kernel"   # chunks run one after another: launch events time one launch
