@@ -1688,8 +1688,15 @@ static bool wide32_ok(const GemmProblem &p) {
 
 // The streamed wide kernel takes every wide-kernel problem whose operator is drawn in the GEMM (a
 // materialised window keeps the 64 x 512 GMAT kernels): same conditions, bitwise the same sums.
+#ifndef RBH_STREAM64
+#define RBH_STREAM64 1   // (variant builds for A/B timing: 0 keeps f64 on the 64 x 512 kernel)
+#endif
+#ifndef RBH_STREAM32
+#define RBH_STREAM32 1
+#endif
 template <typename T>
 static bool stream_ok(const GemmProblem &p) {
+    if (sizeof(T) == 8 ? !RBH_STREAM64 : !RBH_STREAM32) return false;
     return !p.materialise && (sizeof(T) == 8 ? wide_ok<T>(p) : wide32_ok<T>(p));
 }
 
