@@ -1688,8 +1688,12 @@ static bool wide32_ok(const GemmProblem &p) {
 
 // The streamed wide kernel takes every wide-kernel problem whose operator is drawn in the GEMM (a
 // materialised window keeps the 64 x 512 GMAT kernels): same conditions, bitwise the same sums.
+// f64 stays on the 64 x 512 kernel: measured C2 8.72 ms there against 8.92-9.15 ms streamed (PF 1,
+// 3, 7; same box, two alternations). The f64 MFMA is twice as long, so halving the draws saves half
+// as much per MFMA, while the streamed tile doubles the memory loads per MFMA. f32 (C4): 4.71 ms
+// streamed against 4.90-4.94 ms on skge_wide32_kernel.
 #ifndef RBH_STREAM64
-#define RBH_STREAM64 1   // (variant builds for A/B timing: 0 keeps f64 on the 64 x 512 kernel)
+#define RBH_STREAM64 0   // (variant builds for A/B timing: 1 puts f64 on the streamed kernel)
 #endif
 #ifndef RBH_STREAM32
 #define RBH_STREAM32 1

@@ -232,11 +232,12 @@ def _oracle_left(d, n, m, alpha, rows, cols, vals, A, beta, B0, layout="C"):
     return Bexp
 
 
-@pytest.mark.parametrize("d,m,n,vec", [(1024, 16384, 256, 8), (200, 999, 130, 3), (40, 100, 16, 2)])
+@pytest.mark.parametrize("d,m,n,vec", [(1024, 16384, 256, 8), (200, 1000, 130, 3), (40, 100, 16, 2)])
 @pytest.mark.parametrize("alpha", [1.0, -1.0])
 def test_fill_sparse_op_applies_on_dma_path(cuda, d, m, n, vec, alpha):
     """fill_sparse_op(S) once, then two sketches from its arrays (sparse_filled: no host wait):
-    the LDS-DMA apply, bitwise the oracle's; the same arrays passed as a plain user operator (origin
+    the LDS-DMA apply (ColMajor A with an even leading dimension: 16-B panel loads), bitwise the
+    oracle's; the same arrays passed as a plain user operator (origin
     unknown: the call waits for the device check) give the same bits on the same path."""
     A = O.random_matrix(m, n, 99)
     B0 = O.random_matrix(d, n, 42)
