@@ -63,6 +63,8 @@ CONFIGS = {
 
 
 # the timed kernel of each workload kind (its name in the rocprofv3 summaries)
+KERNEL_NAMES = {"stream": "skge_stream_kernel", "wide": "skge_wide_kernel", "wide32": "skge_wide32_kernel",
+                "fused": "skge_fused_kernel", "generic": "skge_gemm_kernel"}
 DOMINANT = {"dense": "skge_", "saso": "saso_dma_kernel", "sksy": "skge_", "sksyp": "skge_"}
 
 
@@ -391,6 +393,14 @@ def main():
     roof["basis"] = per
     roof["traffic"], roof["traffic_source"] = pmc_traffic(args.config)
 
+    # the kernel the dense paths ran (sksy: the sketch on A's full storage, the same plan)
+    plan, kname = None, None
+    if kind in ("dense", "sksy"):
+        pl = rb.plan_left("C", "N", "N", d, n, m, S, A, n if kind == "sksy" else lda, d,
+                          ro_s=rank * d if use_dist else 0, dtype=dtype)
+        plan = {"kernel": pl.kernel, "splitk": pl.splitk, "tiles": pl.tiles, "workgroups": pl.workgroups}
+        kname = KERNEL_NAMES.get(pl.kernel, pl.kernel)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
@@ -438,11 +448,13 @@ def main():
                                        if use_dist else "single GPU")},
             "pct_of_peak": roof["frac"] * 100.0,
             # what kernel_ms and the roofline time; any other launch of the step is in ms_per_step only
-            "dominant_kernel": {"dense": "skge_stream_kernel (one per chunk)",
+            "dominant_kernel": {"dense": f"{kname} (one per chunk)",
                                 "saso": "saso_dma_kernel (sampling and the CSR build: ms_per_step only)",
-                                "sksy": "skge_stream_kernel (the symmetry check, the step's other launch: "
+                                "sksy": f"{kname} (the symmetry check, the step's other launch: "
                                         "ms_per_step only)",
                                 "sksyp": "skge_wide_kernel<TRI 3>"}[kind],
+            # the library's plan of the dense rank problem (rbh_lskge3_plan): kernel, split-K, tiles
+            "plan": plan,
             "roofline": roof,
             "cpu_baseline": cpu,
         }

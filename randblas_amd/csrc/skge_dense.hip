@@ -1149,8 +1149,9 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Streamed wide kernel (round 4): 32 generated x 1024 memory outer indices, the memory operand
-// loaded straight into MFMA fragments, the generated tile through an LDS ring
+// Streamed wide kernel (round 4): BG = 32 (f64, f32) or 64 (f32) generated x 1024 memory outer
+// indices, the memory operand loaded straight into MFMA fragments, the generated tile through an
+// LDS ring
 // ------------------------------------------------------------------------------------------
 // The same sums, in the same order, as skge_wide_kernel (f64) / skge_wide32_kernel (f32): a step
 // covers 128 bytes of K per row (16 f64 / 32 f32 values), lane (g, r) of a 16 x 16 MFMA tile
@@ -1158,36 +1159,41 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
 // steps in ascending k; each output element's MFMA chain is therefore bit for bit the older
 // kernels' (and the one-triangle / materialised kernels', which keep the 64 x 512 tiles).
 // What changes is the data movement:
-//  * Operator draws. The generated tile is 32 rows instead of 64, for the same 1024 x 32 = 64 x 512
-//    accumulator budget, so every operator entry is drawn once per 1024 memory rows instead of per
-//    512: half the Philox + Box-Muller VALU per MFMA (on gfx950 f64 / f32 MFMAs hold their SIMD's
-//    issue, so every VALU instruction adds to the step; tools/micro/mfma_coexec.hip).
+//  * Operator draws. Every operator entry is drawn once per 1024 memory rows instead of per 512:
+//    half the Philox + Box-Muller VALU per MFMA (on gfx950 f64 / f32 MFMAs hold their SIMD's issue,
+//    so every VALU instruction adds to the step; tools/micro/mfma_coexec.hip). BG = 32 keeps the
+//    64 x 512 accumulator budget; f32 BG = 64 doubles it (128 accumulator registers a wave) and
+//    halves the memory loads per MFMA as well (stream_geom chooses).
 //  * No memory tile in LDS. Wave w owns memory rows [128 w, 128 w + 128) of the tile and loads each
 //    lane's 32 B per 16-row block (two 16-B buffer loads) straight into the registers the MFMAs
-//    read: no LDS staging writes, no fragment reads, no barrier for the memory operand. Block c of
-//    step kt + 1 is loaded PF blocks ahead of its use (a ring of PF + 1 register slots).
+//    read: no LDS staging writes, no fragment reads, no barrier for the memory operand. A step runs
+//    as two halves (the lane's first and second 16 B), each 16-B half-block loaded PF half-blocks
+//    ahead of its use (a ring of PF + 1 register slots, across steps).
 //  * One barrier per round of R = 4 steps. The 32 x 128-B generated tiles of a round sit in an LDS
-//    ring (2 rounds x 4 slots, 32 KiB); every wave draws its share of the NEXT round's tiles (f64:
-//    one Philox call per lane and round, f32: two) in the middle of the round, so the draw is
-//    spread evenly over the four SIMDs and the waves meet once per round.
+//    ring (2 rounds x 4 slots, BG x 128 B each); every wave draws its share of the NEXT round's
+//    tiles (Philox calls per lane and round: f64 one, f32 two (BG 32) / four (BG 64)) during the
+//    round, so the draw is spread evenly over the four SIMDs and the waves meet once per round.
 // Requires K % (128 / sizeof(T)) == 0, a memory operand with 16-B aligned rows contiguous along k
 // (mode 2), pc0 % 4 == 0, and the wave's 128 rows addressable with 32-bit byte offsets.
-template <typename T, int GK, int FAMILY, bool GX, bool SPLIT, int PF>
+template <typename T, int GK, int FAMILY, bool GX, bool SPLIT, int PF, int BG>
 __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     constexpr int KS = 128 / (int)sizeof(T);              // k per step
     constexpr int VPL = 32 / (int)sizeof(T);              // k values per lane and step: k = VPL g + v
     constexpr int EPS = 16 / (int)sizeof(T);              // elements per 16-B slot
-    constexpr int BG = 32, BMW = 128;                     // generated rows; memory rows per wave
-    constexpr int FA = BG / 16, FB = BMW / 16;            // 2 x 8 MFMA tiles per wave
+    constexpr int BMW = 128;                              // memory rows per wave
+    constexpr int FA = BG / 16, FB = BMW / 16;            // FA x 8 MFMA tiles per wave
     constexpr int R = 4;                                  // steps per round
-    constexpr int SLOT_B = BG * 128;                      // bytes per generated tile (32 rows x 128 B)
-    constexpr int CPS = BG * KS / 4;                      // Philox calls per step (f64 128, f32 256)
-    constexpr int WCALLS = R * CPS / 512;                 // wave-calls per wave and round (1, 2)
+    constexpr int SLOT_B = BG * 128;                      // bytes per generated tile (BG rows x 128 B)
+    constexpr int CPS = BG * KS / 4;                      // Philox calls per step (f64 128, f32 512)
+    constexpr int SPU = 512 / CPS;                        // steps between a lane's calls of a round
+    constexpr int WCALLS = R / SPU;                       // wave-calls per wave and round (f64 1, f32 4)
+    constexpr int NH = 2 * FB;                            // 16-B half-blocks of a step (h FB + c)
     constexpr int NSLOT = PF + 1;                         // register slots of the memory prefetch ring
-    static_assert(FB % NSLOT == 0, "a block's slot must not depend on the step");
+    static_assert(NH % NSLOT == 0, "a half-block's slot must not depend on the step");
+    static_assert(512 % CPS == 0 && R % SPU == 0, "every lane's calls of a round: same row, steps u SPU + ts0");
     typedef typename Mfma<T>::v4 acc_t;
     typedef float v4f __attribute__((ext_vector_type(4)));
-    typedef T tv_t __attribute__((ext_vector_type(VPL)));   // a lane's VPL values of one row
+    typedef T hv_t __attribute__((ext_vector_type(EPS)));   // 16 B of a lane's VPL values of one row
 
     __shared__ __attribute__((aligned(16))) char gring[2 * R * SLOT_B];
     __shared__ rb::LogfEntry tab[16];
@@ -1226,57 +1232,51 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
         row = row < mnO ? row : mnO - 1;
         voff[c] = (uint32_t)(((row - wbase) * mop.so + (int64_t)VPL * g) * (int64_t)sizeof(T));
     }
-    tv_t mv[NSLOT];
-    auto mload = [&](int slot, int c, int64_t kt) {
+    // a step runs in two halves: half h contracts the lane's values v = EPS h .. EPS h + EPS - 1 (its
+    // 16-B slot 2 g + h), so a fragment is one 16-B load and the ring holds half-blocks
+    hv_t mv[NSLOT];
+    auto mload = [&](int slot, int i, int64_t kt) {   // half-block i = h FB + c of step kt
         const uint32_t soff = (uint32_t)(kt * 128);
-        const v4f lo = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(mrsrc, voff[c], soff, 0));
-        const v4f hi = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(mrsrc, voff[c] + 16u, soff, 0));
-        typedef float v8f __attribute__((ext_vector_type(8)));
-        v8f both;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { both[e] = lo[e]; both[4 + e] = hi[e]; }
-        mv[slot] = __builtin_bit_cast(tv_t, both);
+        mv[slot] = __builtin_bit_cast(hv_t, __builtin_amdgcn_raw_buffer_load_b128(mrsrc, voff[i % FB] + 16u * (i / FB), soff, 0));
     };
 
     // ---- generated operand: slot (ring half, step t) holds rows o < 32 of 8 16-B slots each, slot q
     // of row o at q ^ sw32(o) (conflict-free ds_read_b128 fragment reads, as in skge_wide32_kernel)
     auto gslot = [&](int half, int ts) -> char * { return gring + (half * R + ts) * SLOT_B; };
-    // this lane's Philox calls of a round: call u covers step ts_u, call cc_u of that step
-    uint32_t cbase[WCALLS][4];
-    int ts_of[WCALLS], cc_of[WCALLS];
-#pragma unroll
-    for (int u = 0; u < WCALLS; ++u) {
-        const int c = 64 * wave + lane + 512 * u;
-        ts_of[u] = c / CPS;
-        cc_of[u] = c % CPS;
-        uint64_t off;
-        if (GK == GEN_OK) {   // call = (row o, k quad qd)
-            const int o = cc_of[u] / (KS / 4), qd = cc_of[u] % (KS / 4);
-            off = (uint64_t)(gop.pr0 + go0 + o) * gop.stride + (uint64_t)(gop.pc0 >> 2) + (uint64_t)ts_of[u] * (KS / 4) + qd;
-        } else {              // call = (k, row quad qo)
-            const int k = cc_of[u] / (BG / 4), qo = cc_of[u] % (BG / 4);
-            off = (uint64_t)(gop.pr0 + (int64_t)ts_of[u] * KS + k) * gop.stride + (uint64_t)((gop.pc0 + go0) >> 2) + qo;
-        }
-        rb::ctr_add(gop.ctr, off, cbase[u]);
-    }
+    // this lane's Philox calls of a round: call u is call cc of step ts0 + u SPU (the flat call index
+    // 64 wave + lane + 512 u of the round, CPS calls per step)
+    const int ts0 = (64 * wave + lane) / CPS, cc = (64 * wave + lane) % CPS;
     // counter advance per step: GEN_OK KS / 4 quads, GEN_OO KS natural rows
     const uint64_t cstep = GK == GEN_OK ? (uint64_t)(KS / 4) : (uint64_t)KS * gop.stride;
+    uint32_t cbase[4];   // call cc of step 0
+    {
+        uint64_t off;
+        if (GK == GEN_OK) {   // call = (row o, k quad qd)
+            const int o = cc / (KS / 4), qd = cc % (KS / 4);
+            off = (uint64_t)(gop.pr0 + go0 + o) * gop.stride + (uint64_t)(gop.pc0 >> 2) + qd;
+        } else {              // call = (k, row quad qo)
+            const int k = cc / (BG / 4), qo = cc % (BG / 4);
+            off = (uint64_t)(gop.pr0 + k) * gop.stride + (uint64_t)((gop.pc0 + go0) >> 2) + qo;
+        }
+        rb::ctr_add(gop.ctr, off, cbase);
+    }
     const bool gtile_full = go0 + BG <= gnO;
     // draw call u of the round starting at step kr0 into ring half `half` (steps >= kend: nothing)
     auto draw = [&](int u, int64_t kr0, int half, int64_t kend) {
-        const int64_t kt = kr0 + ts_of[u];
-        if (kt >= kend) return;   // (uniform per wave: ts_of is per wave for CPS >= 64)
-        uint32_t cc[4];
-        rb::ctr_add(cbase[u], (uint64_t)kr0 * cstep, cc);
-        const rb::u32x4 w = rb::philox4x32_uk<10>(cc[0], cc[1], cc[2], cc[3], gop.key[0], gop.key[1]);
+        const int ts = ts0 + u * SPU;
+        const int64_t kt = kr0 + ts;
+        if (kt >= kend) return;   // (uniform per wave: ts0 is per wave for CPS >= 64)
+        uint32_t ct[4];
+        rb::ctr_add(cbase, (uint64_t)kt * cstep, ct);
+        const rb::u32x4 w = rb::philox4x32_uk<10>(ct[0], ct[1], ct[2], ct[3], gop.key[0], gop.key[1]);
         float sm[4];
         rb::sample4<FAMILY>(w, sm, tab);
         T v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = FAMILY == rb::UNIFORM ? (T)sm[e] * (T)gop.scale : (T)sm[e];
-        char *G = gslot(half, ts_of[u]);
+        char *G = gslot(half, ts);
         if (GK == GEN_OK) {
-            const int o = cc_of[u] / (KS / 4), qd = cc_of[u] % (KS / 4);
+            const int o = cc / (KS / 4), qd = cc % (KS / 4);
             if (!gtile_full && go0 + o >= gnO) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) v[e] = (T)0;
@@ -1290,7 +1290,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
                 for (int e = 0; e < EPS; ++e) dst[e] = v[hsl * EPS + e];
             }
         } else {
-            const int k = cc_of[u] / (BG / 4), qo = cc_of[u] % (BG / 4);
+            const int k = cc / (BG / 4), qo = cc % (BG / 4);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int o = 4 * qo + e;
@@ -1299,16 +1299,10 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
             }
         }
     };
-    // a lane's generated fragment of row 16 a + r for the step in slot (half, ts): slots 2 g, 2 g + 1
-    auto gread = [&](int half, int ts, int a) -> tv_t {
+    // a lane's generated fragment of row 16 a + r, half h, for the step in slot (half, ts): slot 2 g + h
+    auto gread = [&](int half, int ts, int a, int h) -> hv_t {
         const char *G = gslot(half, ts) + (16 * a + r) * 128;
-        const v4f lo = *reinterpret_cast<const v4f *>(G + 16 * ((2 * g) ^ sw32(r)));
-        const v4f hi = *reinterpret_cast<const v4f *>(G + 16 * ((2 * g + 1) ^ sw32(r)));
-        typedef float v8f __attribute__((ext_vector_type(8)));
-        v8f both;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { both[e] = lo[e]; both[4 + e] = hi[e]; }
-        return __builtin_bit_cast(tv_t, both);
+        return *reinterpret_cast<const hv_t *>(G + 16 * ((2 * g + h) ^ sw32(r)));
     };
 
     acc_t acc[FA][FB];
@@ -1326,7 +1320,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     for (int u = 0; u < WCALLS; ++u) draw(u, kt0, 0, kt1);
     if (kt0 < kt1) {
 #pragma unroll
-        for (int c = 0; c < PF; ++c) mload(c % NSLOT, c, kt0);
+        for (int i = 0; i < PF; ++i) mload(i % NSLOT, i, kt0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
@@ -1338,24 +1332,27 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
         for (int ts = 0; ts < R; ++ts) {
             const int64_t kt = kr0 + ts;
             if (kt >= kt1) break;
-            tv_t gf[FA];
 #pragma unroll
-            for (int a = 0; a < FA; ++a) gf[a] = gread(half, ts, a);
+            for (int h = 0; h < 2; ++h) {
+                hv_t gf[FA];
 #pragma unroll
-            for (int c = 0; c < FB; ++c) {
-                // block c + PF (this step's, or the next step's first blocks), PF blocks ahead
-                const int cn = c + PF;
-                const int64_t ktn = cn < FB ? kt : (kt + 1 < kt1 ? kt + 1 : kt);
-                mload(cn % NSLOT, cn % FB, ktn);
-                const tv_t &m = mv[c % NSLOT];
+                for (int a = 0; a < FA; ++a) gf[a] = gread(half, ts, a, h);
 #pragma unroll
-                for (int v = 0; v < VPL; ++v)
+                for (int c = 0; c < FB; ++c) {
+                    // half-block i + PF (this step's, or the next step's first ones), PF ahead
+                    const int i = h * FB + c, in = i + PF;
+                    const int64_t ktn = in < NH ? kt : (kt + 1 < kt1 ? kt + 1 : kt);
+                    mload(in % NSLOT, in % NH, ktn);
+                    const hv_t &m = mv[i % NSLOT];
 #pragma unroll
-                    for (int a = 0; a < FA; ++a)
-                        acc[a][c] = GX ? Mfma<T>::mma(m[v], gf[a][v], acc[a][c]) : Mfma<T>::mma(gf[a][v], m[v], acc[a][c]);
+                    for (int e = 0; e < EPS; ++e)
+#pragma unroll
+                        for (int a = 0; a < FA; ++a)
+                            acc[a][c] = GX ? Mfma<T>::mma(m[e], gf[a][e], acc[a][c]) : Mfma<T>::mma(gf[a][e], m[e], acc[a][c]);
+                }
             }
             // the next round's generated tiles: every wave's share, spread over the round (f64: its
-            // one call after step 1; f32: after steps 0 and 2)
+            // one call after step 1; f32: one call after every step)
             if (rd + 1 < nrounds) {
 #pragma unroll
                 for (int u = 0; u < WCALLS; ++u)
@@ -1634,14 +1631,47 @@ static bool wide_ok(const GemmProblem &p) {
     return sizeof(T) == 8 && fused_ok(p) && p.K % BK == 0 && wide_offsets_ok<T>(p);
 }
 
+// f32 streamed tile height: 64 (64 x 1024 tiles, 128 accumulator registers) where stream_geom picks
+// it; 32 forces the 32 x 1024 tiles everywhere (variant builds for A/B timing)
+#ifndef RBH_STREAM_BG32
+#define RBH_STREAM_BG32 64
+#endif
+// Streamed-kernel geometry: the generated tile height BG and the split-K factor, which the f32
+// materialised path (skge_wide32_kernel) shares so that both give the same bits. f64: BG = 32, the
+// split of the 64 x 512 kernels. f32: BG = 64 (every loaded memory value feeds four MFMA tiles;
+// measured 80.5 % of peak against 74.6 % for BG = 32 at d = 1024 / 512, m = n = 16384 / 32768) unless
+// its half as many tiles leave the chip emptier: the choice minimises (workgroup waves) x (work per
+// workgroup), BG = 64 work priced at 0.93 of BG = 32's per row (that measurement). C4 (d = 256,
+// 128 tiles of 64 x 1024) takes BG = 64 with split 2 (256 workgroups).
+struct StreamGeom {
+    int bg;
+    int split;
+};
+constexpr double STREAM_BG64_COST = 0.93;
+template <typename T>
+static StreamGeom stream_geom(const GemmProblem &p) {
+    const bool gx = p.xkind != MEM;
+    const int64_t gnO = gx ? p.M : p.N, mnO = gx ? p.N : p.M;
+    const int64_t nk = p.K / BK;   // 16-deep steps, as the 64 x 512 kernels count them
+    const int64_t wide = ((gnO + 63) / 64) * ((mnO + 511) / 512);
+    const int s32 = choose_split(wide, nk, p.split_req);
+    if (sizeof(T) == 8 || RBH_STREAM_BG32 != 64) return {32, s32};
+    const int64_t t64 = ((gnO + 63) / 64) * ((mnO + 1023) / 1024), t32 = ((gnO + 31) / 32) * ((mnO + 1023) / 1024);
+    const int s64 = choose_split(t64, nk, p.split_req);
+    const int64_t cus = device_cus();
+    const double c32 = (double)((t32 * s32 + cus - 1) / cus) * 32.0 / s32;
+    const double c64 = (double)((t64 * s64 + cus - 1) / cus) * 64.0 * STREAM_BG64_COST / s64;
+    return c64 < c32 ? StreamGeom{64, s64} : StreamGeom{32, s32};
+}
+
 template <int GK, int FAMILY, bool GX>
 static hipError_t launch_wide32(const GemmProblem &p, hipStream_t s) {
     typedef float T;
     const int64_t gnO = GX ? p.M : p.N, mnO = GX ? p.N : p.M;
     const int64_t nb = ((gnO + 63) / 64) * ((mnO + 511) / 512);
     if (nb <= 0) return hipSuccess;
-    // split-K on the same terms as the 16-deep kernels (the split counts 16-deep steps)
-    const int split = choose_split(nb, p.K / BK, p.split_req);
+    // split-K: the streamed kernel's (stream_geom), so a materialised window gives its bits
+    const int split = stream_geom<T>(p).split;
     GemmProblem q = p;
     q.splitk = split;
     q.partial = nullptr;
@@ -1704,24 +1734,22 @@ static bool stream_ok(const GemmProblem &p) {
     return !p.materialise && (sizeof(T) == 8 ? wide_ok<T>(p) : wide32_ok<T>(p));
 }
 
-// memory blocks loaded ahead of their use (a register ring of PF + 1 blocks); f64 is register-bound
+// 16-B half-blocks loaded ahead of their use (a register ring of PF + 1; PF + 1 divides 16)
 #ifndef RBH_STREAM_PF64
-#define RBH_STREAM_PF64 3
+#define RBH_STREAM_PF64 7
 #endif
 #ifndef RBH_STREAM_PF32
-#define RBH_STREAM_PF32 7
+#define RBH_STREAM_PF32 3
 #endif
 template <typename T> constexpr int stream_pf() { return sizeof(T) == 8 ? RBH_STREAM_PF64 : RBH_STREAM_PF32; }
 
 template <typename T, int GK, int FAMILY, bool GX>
 static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
     const int64_t gnO = GX ? p.M : p.N, mnO = GX ? p.N : p.M;
-    const int64_t nb = ((gnO + 31) / 32) * ((mnO + 1023) / 1024);
+    const StreamGeom gm = stream_geom<T>(p);
+    const int64_t nb = ((gnO + gm.bg - 1) / gm.bg) * ((mnO + 1023) / 1024);
     if (nb <= 0) return hipSuccess;
-    // the split of the 64 x 512 kernels (their tile count, 16-deep steps), so a materialised
-    // window, which runs them, gives the same bits
-    const int64_t nb_wide = ((gnO + 63) / 64) * ((mnO + 511) / 512);
-    const int split = choose_split(nb_wide, p.K / BK, p.split_req);
+    const int split = gm.split;
     GemmProblem q = p;
     q.splitk = split;
     q.partial = nullptr;
@@ -1731,12 +1759,15 @@ static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
         if (e != hipSuccess) return e;
     }
     timing_begin(s);
-    if (split > 1)
-        hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, stream_pf<T>()>), dim3((unsigned)(nb * split)),
-                           dim3(512), 0, s, q);
-    else
-        hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, stream_pf<T>()>), dim3((unsigned)nb), dim3(512), 0,
-                           s, q);
+    const dim3 grid((unsigned)(nb * split));
+    constexpr int BGW = sizeof(T) == 4 ? 64 : 32;   // (f64 never takes BG = 64: 256 accumulator registers)
+    if (gm.bg == 64) {
+        if (split > 1) hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, stream_pf<T>(), BGW>), grid, dim3(512), 0, s, q);
+        else hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, stream_pf<T>(), BGW>), grid, dim3(512), 0, s, q);
+    } else {
+        if (split > 1) hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, stream_pf<T>(), 32>), grid, dim3(512), 0, s, q);
+        else hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, stream_pf<T>(), 32>), grid, dim3(512), 0, s, q);
+    }
     e = hipGetLastError();
     if (split > 1 && e == hipSuccess) {
         hipLaunchKernelGGL(splitk_reduce_kernel<T>, dim3(2048), dim3(256), 0, s, p.M, p.N, split,
@@ -1823,9 +1854,10 @@ static GemmPlan plan_gemm(const GemmProblem &p) {
     } else if (stream_ok<T>(p)) {
         const bool gx = p.xkind != MEM;
         const int64_t gnO = gx ? p.M : p.N, mnO = gx ? p.N : p.M;
+        const StreamGeom gm = stream_geom<T>(p);   // as launch_stream
         pl.kernel = PLAN_STREAM;
-        pl.tiles = ((gnO + 31) / 32) * ((mnO + 1023) / 1024);
-        pl.splitk = choose_split(wide_tiles(), p.K / BK, p.split_req);   // as launch_stream
+        pl.tiles = ((gnO + gm.bg - 1) / gm.bg) * ((mnO + 1023) / 1024);
+        pl.splitk = gm.split;
     } else if (wide_ok<T>(p)) {
         pl.kernel = PLAN_WIDE;
         pl.tiles = wide_tiles();
@@ -1833,7 +1865,7 @@ static GemmPlan plan_gemm(const GemmProblem &p) {
     } else if (wide32_ok<T>(p)) {
         pl.kernel = PLAN_WIDE32;
         pl.tiles = wide_tiles();
-        pl.splitk = choose_split(pl.tiles, p.K / BK, p.split_req);
+        pl.splitk = stream_geom<T>(p).split;   // as launch_wide32
     } else if (fused_ok(p)) {
         constexpr bool F32 = sizeof(T) == 4;
         constexpr int64_t TG = F32 ? 64 : 128, TMW = F32 ? 512 : 256;

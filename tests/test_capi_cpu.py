@@ -122,15 +122,22 @@ def _plan(d, n, m, D_rows=None, ro=0, dtype="f64", opts=None, layout="C"):
 
 
 def test_plan_baseline_configs():
-    # C2 (512 wide tiles) and C4 per GPU (256): full grids, no split
+    # C2 (512 wide tiles): a full grid, no split
     assert _plan(1024, 16384, 16384) == rb.Plan("wide", 1, 512, 512)
-    assert _plan(256, 32768, 32768, D_rows=2048, ro=1792, dtype="f32") == rb.Plan("stream", 1, 256, 256)
+    # C4 per GPU: 128 streamed 64 x 1024 tiles, split 2 (priced below 256 unsplit 32 x 1024 tiles)
+    assert _plan(256, 32768, 32768, D_rows=2048, ro=1792, dtype="f32") == rb.Plan("stream", 2, 128, 256)
+    # f32 at C2's shape: 256 tiles of 64 x 1024 fill the chip once (32 x 1024 would take two waves)
+    assert _plan(1024, 16384, 16384, dtype="f32") == rb.Plan("stream", 1, 256, 256)
+    # too little K to split: 256 tiles of 32 x 1024 beat 128 of 64 x 1024
+    assert _plan(256, 32768, 1024, dtype="f32") == rb.Plan("stream", 1, 256, 256)
     # C1: 16 tiles -> 16 slices of K = 4096
     assert _plan(128, 4096, 4096) == rb.Plan("wide", 16, 16, 256)
     # the north star split over 8 ranks: 128 tiles fill half the chip -> split 2
     assert _plan(256, 16384, 16384, D_rows=2048, ro=1792) == rb.Plan("wide", 2, 128, 256)
-    # a quarter of C4's rank columns alone would split 4: the sharded driver passes the whole split
-    assert _plan(256, 8192, 32768, D_rows=2048, ro=1792, dtype="f32") == rb.Plan("stream", 4, 64, 256)
+    # a quarter of C4's rank columns alone would split 8: the sharded driver passes the whole split
+    assert _plan(256, 8192, 32768, D_rows=2048, ro=1792, dtype="f32") == rb.Plan("stream", 8, 32, 256)
+    assert _plan(256, 8192, 32768, D_rows=2048, ro=1792, dtype="f32",
+                 opts=rb.Options(splitk=2)) == rb.Plan("stream", 2, 64, 128)
     # K below 2048 never splits (every kernel then adds in the same order)
     assert _plan(128, 4096, 1024).splitk == 1
 
@@ -144,7 +151,8 @@ def test_plan_options_fix_the_split():
     assert _plan(1024, 16384, 16384, layout="R").kernel == "generic"
     # the materialised window: the 64 x 512 kernels that load it (the same sums)
     assert _plan(1024, 16384, 16384, opts=rb.Options(materialise=True)).kernel == "wide"
-    assert _plan(256, 32768, 32768, dtype="f32", opts=rb.Options(materialise=True)).kernel == "wide32"
+    # (the f32 materialised kernel takes the streamed kernel's split: the same bits)
+    assert _plan(256, 32768, 32768, dtype="f32", opts=rb.Options(materialise=True)) == rb.Plan("wide32", 2, 256, 512)
     # f32 with K not a multiple of 32: the fused kernel
     assert _plan(256, 4096, 4004, dtype="f32").kernel == "fused"
     with pytest.raises(rb.RandBLASError) as ei:

@@ -332,8 +332,8 @@ def test_wide_split_k_within_bound(cuda, dtype, kernel, layout, opA, split):
 
 def test_f32_split_chunks_bitwise_with_whole_split(cuda):
     """Column chunks computed with the whole problem's split (what RowShardedSketch's
-    dense_rank_compute does: 32 tiles -> split 8) give the unchunked call's bits, although a
-    chunk of 1024 columns alone (8 tiles) would split 32."""
+    dense_rank_compute does: 16 streamed 64 x 1024 tiles -> split 16) give the unchunked call's
+    bits, although a chunk of 1024 columns alone (4 tiles) would split 32."""
     from randblas_amd.distributed import dense_rank_compute
 
     d, m, n = 256, 8192, 4096
@@ -342,7 +342,7 @@ def test_f32_split_chunks_bitwise_with_whole_split(cuda):
     ref = torch.empty(d * n, dtype=torch.float32, device=cuda)
     rb.sketch_general_left("C", "N", "N", d, n, m, 1.0, S, A, m, 0.0, ref, d, ro_s=1792)
     whole = rb.plan_left("C", "N", "N", d, n, m, S, A, m, d, ro_s=1792, dtype="f32")
-    assert whole.kernel == "stream" and whole.splitk == 8, whole   # 32 tiles -> 256 / 32
+    assert whole == rb.Plan("stream", 16, 16, 256), whole   # 16 tiles -> 256 / 16
     comp = dense_rank_compute(S, A, m, m, d, n)
     B = torch.empty_like(ref)
     for j0, j1 in ((0, 1024), (1024, 2048), (2048, 3072), (3072, 4096)):
@@ -351,16 +351,21 @@ def test_f32_split_chunks_bitwise_with_whole_split(cuda):
     assert np.array_equal(got.view(np.uint32), exp.view(np.uint32))
 
 
-# The streamed wide kernel (32 x 1024 tiles, memory operand straight to registers) adds every output
-# element's terms in the same MFMA order as the 64 x 512 wide kernels, which the materialised-window
-# option still runs: bitwise equal across operand orientations (left/right x layouts: the generated
-# operand as X or Y), counter directions (major axis), families, ragged tiles and split-K.
+# The streamed wide kernel (32 or 64 x 1024 tiles, memory operand straight to registers) adds every
+# output element's terms in the same MFMA order as the 64 x 512 wide kernels, which the
+# materialised-window option still runs: bitwise equal across operand orientations (left/right x
+# layouts: the generated operand as X or Y), counter directions (major axis), families, ragged tiles,
+# split-K, and both streamed tile heights (f32 "bg64": 64 x 1024 tiles unsplit, "bg64split": split 16).
+STREAM_SHAPES = {"ragged": (100, 2100, 256), "split": (64, 1100, 4096), "bg64": (1000, 9000, 256),
+                 "bg64split": (250, 4000, 4096)}
+
+
 @pytest.mark.parametrize("dtype", [np.float32])
 @pytest.mark.parametrize("side,layout", [("L", "C"), ("L", "R"), ("R", "C"), ("R", "R")])
 @pytest.mark.parametrize("fam,maj", [("G", "L"), ("G", "S"), ("U", "L")])
-@pytest.mark.parametrize("shape", ["ragged", "split"])
+@pytest.mark.parametrize("shape", sorted(STREAM_SHAPES))
 def test_stream_kernel_equals_wide_bitwise(cuda, dtype, side, layout, fam, maj, shape):
-    d, n, m = (100, 2100, 256) if shape == "ragged" else (64, 1100, 4096)
+    d, n, m = STREAM_SHAPES[shape]
     tag = "f64" if dtype == np.float64 else "f32"
     ut = np.uint64 if dtype == np.float64 else np.uint32
     out, plans = [], []
@@ -387,7 +392,9 @@ def test_stream_kernel_equals_wide_bitwise(cuda, dtype, side, layout, fam, maj, 
                                     co_s=4, options=opts)
         out.append(host(B))
     assert plans[0].kernel == "stream" and plans[1].kernel in ("wide", "wide32"), plans
-    assert plans[0].splitk == plans[1].splitk and (shape == "ragged" or plans[0].splitk > 1), plans
+    assert plans[0].splitk == plans[1].splitk and (plans[0].splitk > 1) == shape.endswith("split"), plans
+    bg = 64 if shape.startswith("bg64") else 32
+    assert plans[0].tiles == -(-(d) // bg) * -(-n // 1024), plans
     assert np.array_equal(out[0].view(ut), out[1].view(ut)), f"{np.sum(out[0] != out[1])} differ"
 
 

@@ -1,0 +1,54 @@
+"""Time B = S A (sketch_general_left, Gaussian DenseSkOp) at an arbitrary shape and dtype: the average
+of --reps calls between two HIP events after --warmup calls. For A/B timing of library variants
+(RBH_LIB_PATH) at shapes outside bench.py's configs. Prints one JSON line.
+Usage: python tools/time_dense.py --dtype f32 --d 1024 --m 16384 --n 16384"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import randblas_amd as rb  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dtype", default="f32", choices=["f32", "f64"])
+    ap.add_argument("--d", type=int, default=1024)
+    ap.add_argument("--m", type=int, default=16384)
+    ap.add_argument("--n", type=int, default=16384)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    tdt = torch.float64 if a.dtype == "f64" else torch.float32
+    A = torch.empty(a.m * a.n, dtype=tdt, device=dev)
+    rb.fill_dense("C", rb.DenseDist(a.m, a.n), a.m, a.n, 0, 0, A, rb.RNGState(99))
+    S = rb.DenseSkOp(rb.DenseDist(a.d, a.m), rb.RNGState(0))
+    B = torch.empty(a.d * a.n, dtype=tdt, device=dev)
+
+    def call():
+        rb.sketch_general_left("C", "N", "N", a.d, a.n, a.m, 1.0, S, A, a.m, 0.0, B, a.d)
+
+    for _ in range(a.warmup):
+        call()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(a.reps):
+        call()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / a.reps
+    plan = rb.plan_left("C", "N", "N", a.d, a.n, a.m, S, A, a.m, a.d, dtype=a.dtype)
+    flops = 2.0 * a.d * a.m * a.n
+    peak = 78.6e12 if a.dtype == "f64" else 157.3e12
+    print(json.dumps({"dtype": a.dtype, "d": a.d, "m": a.m, "n": a.n, "ms": ms, "tflops": flops / ms / 1e9,
+                      "frac": flops / ms / 1e-3 / peak, "plan": plan.kernel, "tiles": plan.tiles,
+                      "splitk": plan.splitk}))
+
+
+if __name__ == "__main__":
+    main()
