@@ -1166,9 +1166,10 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
 //    halves the memory loads per MFMA as well (stream_geom chooses).
 //  * No memory tile in LDS. Wave w owns memory rows [128 w, 128 w + 128) of the tile and loads each
 //    lane's 32 B per 16-row block (two 16-B buffer loads) straight into the registers the MFMAs
-//    read: no LDS staging writes, no fragment reads, no barrier for the memory operand. A step runs
-//    as two halves (the lane's first and second 16 B), each 16-B half-block loaded PF half-blocks
-//    ahead of its use (a ring of PF + 1 register slots, across steps).
+//    read: no LDS staging writes, no fragment reads, no barrier for the memory operand. Each block
+//    is loaded PF blocks ahead of its use (a ring of PF + 1 register slots, across steps); with
+//    BG = 64 a step runs as two parts (the lane's first and second 16 B), which halves the fragment
+//    and ring registers beside the 128 accumulators.
 //  * One barrier per round of R = 4 steps. The 32 x 128-B generated tiles of a round sit in an LDS
 //    ring (2 rounds x 4 slots, BG x 128 B each); every wave draws its share of the NEXT round's
 //    tiles (Philox calls per lane and round: f64 one, f32 two (BG 32) / four (BG 64)) during the
@@ -1187,13 +1188,19 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     constexpr int CPS = BG * KS / 4;                      // Philox calls per step (f64 128, f32 512)
     constexpr int SPU = 512 / CPS;                        // steps between a lane's calls of a round
     constexpr int WCALLS = R / SPU;                       // wave-calls per wave and round (f64 1, f32 4)
-    constexpr int NH = 2 * FB;                            // 16-B half-blocks of a step (h FB + c)
+    // a step runs in NPART parts: BG = 64 in two (each the lane's next 16 B: half the fragment
+    // registers, for the 128 accumulators), BG = 32 in one (the lane's 32 B)
+    constexpr int NPART = BG == 64 ? 2 : 1;
+    constexpr int PV = VPL / NPART;                       // values per lane and part
+    constexpr int NLD = 2 / NPART;                        // 16-B loads per part fragment
+    constexpr int NH = NPART * FB;                        // part-blocks of a step (part FB + c)
     constexpr int NSLOT = PF + 1;                         // register slots of the memory prefetch ring
-    static_assert(NH % NSLOT == 0, "a half-block's slot must not depend on the step");
+    static_assert(NH % NSLOT == 0, "a part-block's slot must not depend on the step");
     static_assert(512 % CPS == 0 && R % SPU == 0, "every lane's calls of a round: same row, steps u SPU + ts0");
     typedef typename Mfma<T>::v4 acc_t;
     typedef float v4f __attribute__((ext_vector_type(4)));
-    typedef T hv_t __attribute__((ext_vector_type(EPS)));   // 16 B of a lane's VPL values of one row
+    typedef T hv_t __attribute__((ext_vector_type(PV)));    // a part of a lane's VPL values of one row
+    typedef float pf_t __attribute__((ext_vector_type(4 * NLD)));
 
     __shared__ __attribute__((aligned(16))) char gring[2 * R * SLOT_B];
     __shared__ rb::LogfEntry tab[16];
@@ -1232,12 +1239,20 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
         row = row < mnO ? row : mnO - 1;
         voff[c] = (uint32_t)(((row - wbase) * mop.so + (int64_t)VPL * g) * (int64_t)sizeof(T));
     }
-    // a step runs in two halves: half h contracts the lane's values v = EPS h .. EPS h + EPS - 1 (its
-    // 16-B slot 2 g + h), so a fragment is one 16-B load and the ring holds half-blocks
+    // part p contracts the lane's values v = PV p .. PV p + PV - 1 (its 16-B slots 2 g + NLD p + l,
+    // l < NLD); the ring holds part-blocks
     hv_t mv[NSLOT];
-    auto mload = [&](int slot, int i, int64_t kt) {   // half-block i = h FB + c of step kt
+    auto mload = [&](int slot, int i, int64_t kt) {   // part-block i = p FB + c of step kt
         const uint32_t soff = (uint32_t)(kt * 128);
-        mv[slot] = __builtin_bit_cast(hv_t, __builtin_amdgcn_raw_buffer_load_b128(mrsrc, voff[i % FB] + 16u * (i / FB), soff, 0));
+        pf_t x;
+#pragma unroll
+        for (int l = 0; l < NLD; ++l) {
+            const v4f y = __builtin_bit_cast(
+                v4f, __builtin_amdgcn_raw_buffer_load_b128(mrsrc, voff[i % FB] + 16u * (NLD * (i / FB) + l), soff, 0));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[4 * l + e] = y[e];
+        }
+        mv[slot] = __builtin_bit_cast(hv_t, x);
     };
 
     // ---- generated operand: slot (ring half, step t) holds rows o < 32 of 8 16-B slots each, slot q
@@ -1300,9 +1315,16 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
         }
     };
     // a lane's generated fragment of row 16 a + r, half h, for the step in slot (half, ts): slot 2 g + h
-    auto gread = [&](int half, int ts, int a, int h) -> hv_t {
+    auto gread = [&](int half, int ts, int a, int p) -> hv_t {
         const char *G = gslot(half, ts) + (16 * a + r) * 128;
-        return *reinterpret_cast<const hv_t *>(G + 16 * ((2 * g + h) ^ sw32(r)));
+        pf_t x;
+#pragma unroll
+        for (int l = 0; l < NLD; ++l) {
+            const v4f y = *reinterpret_cast<const v4f *>(G + 16 * ((2 * g + NLD * p + l) ^ sw32(r)));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[4 * l + e] = y[e];
+        }
+        return __builtin_bit_cast(hv_t, x);
     };
 
     acc_t acc[FA][FB];
@@ -1333,19 +1355,19 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
             const int64_t kt = kr0 + ts;
             if (kt >= kt1) break;
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
+            for (int h = 0; h < NPART; ++h) {
                 hv_t gf[FA];
 #pragma unroll
                 for (int a = 0; a < FA; ++a) gf[a] = gread(half, ts, a, h);
 #pragma unroll
                 for (int c = 0; c < FB; ++c) {
-                    // half-block i + PF (this step's, or the next step's first ones), PF ahead
+                    // part-block i + PF (this step's, or the next step's first ones), PF ahead
                     const int i = h * FB + c, in = i + PF;
                     const int64_t ktn = in < NH ? kt : (kt + 1 < kt1 ? kt + 1 : kt);
                     mload(in % NSLOT, in % NH, ktn);
                     const hv_t &m = mv[i % NSLOT];
 #pragma unroll
-                    for (int e = 0; e < EPS; ++e)
+                    for (int e = 0; e < PV; ++e)
 #pragma unroll
                         for (int a = 0; a < FA; ++a)
                             acc[a][c] = GX ? Mfma<T>::mma(m[e], gf[a][e], acc[a][c]) : Mfma<T>::mma(gf[a][e], m[e], acc[a][c]);
@@ -1734,9 +1756,9 @@ static bool stream_ok(const GemmProblem &p) {
     return !p.materialise && (sizeof(T) == 8 ? wide_ok<T>(p) : wide32_ok<T>(p));
 }
 
-// 16-B half-blocks loaded ahead of their use (a register ring of PF + 1; PF + 1 divides 16)
+// part-blocks loaded ahead of their use (a register ring of PF + 1; PF + 1 divides 8)
 #ifndef RBH_STREAM_PF64
-#define RBH_STREAM_PF64 7
+#define RBH_STREAM_PF64 3
 #endif
 #ifndef RBH_STREAM_PF32
 #define RBH_STREAM_PF32 3

@@ -21,6 +21,12 @@ stream waits for it), and the unpack waits for the gather on the exchange stream
 the slot only after step s's exchange has finished. Only the last step's exchange is left after
 the last compute; wait() (or a device synchronisation) joins it.
 
+Direct gathers. Where the gathered shards already form B's layout -- column shards in one chunk
+(rank g's d x n_loc ColMajor block sits at g n_loc d), or a single rank holding every row -- the
+all-gather writes B_full itself and no unpack copy runs. A single rank with one chunk computes
+straight into B_full and gathers in place (input = output: RCCL moves nothing), so its step costs
+the compute alone; the next step's compute then waits for that gather.
+
 Bitwise results. A rank's shard is one library call over all its columns by default (chunks = 1),
 so it is bit for bit the call a single GPU makes for those rows (and, while no split-K engages,
 for any world size: the wide kernels add each output element's k terms in an order that does not
@@ -88,16 +94,25 @@ class _Pipeline:
         self.cuda = device.type == "cuda"
         self.local = [[torch.empty(shard_elems(j1 - j0), dtype=dtype, device=device) for j0, j1 in cols]
                       for _ in range(self.SLOTS)]
-        self.gathered = [[torch.empty(self.world * shard_elems(j1 - j0), dtype=dtype, device=device)
-                          for j0, j1 in cols] for _ in range(self.SLOTS)] if self.dist else None
+        self._shard_elems, self._dtype, self._device = shard_elems, dtype, device
+        self._gathered = {}   # (slot, chunk) -> gather buffer, made on first use (direct gathers need none)
         self.xs = torch.cuda.Stream(device) if self.cuda else None   # exchange (unpack) stream
         # gloo with device tensors: the collective runs on host copies of the shards
         self.host_gather = self.dist and self.cuda and dist.get_backend(group) == "gloo"
         self.slot_free: List[Optional[torch.cuda.Event]] = [None] * self.SLOTS
         self.steps = 0
+        self.pending = None   # the last in-place all-gather (_step_in_place)
         # timing (CUDA only): per step (start, compute done) on the compute stream
         self.timing = False
         self.marks: List = []
+
+    def gathered(self, slot: int, c: int) -> torch.Tensor:
+        key = (slot, c)
+        if key not in self._gathered:
+            j0, j1 = self.cols[c]
+            self._gathered[key] = torch.empty(self.world * self._shard_elems(j1 - j0), dtype=self._dtype,
+                                              device=self._device)
+        return self._gathered[key]
 
     def _ev(self, stream):
         e = torch.cuda.Event(enable_timing=True)
@@ -110,10 +125,19 @@ class _Pipeline:
     def _unpack_chunk(self, c: int, j0: int, j1: int, src: torch.Tensor, B_full: torch.Tensor) -> None:
         raise NotImplementedError
 
+    def _direct(self, B_full: torch.Tensor) -> Optional[torch.Tensor]:
+        """The span of B_full that the gathered shards of the (single) chunk form exactly as they
+        arrive (the ranks' blocks in rank order), or None when they need the unpack copy."""
+        return None
+
     def __call__(self, B_full: Optional[torch.Tensor]) -> None:
         """Enqueue one step: compute this rank's shard; with B_full, all-gather and reassemble the
         whole sketch into it on every rank (on the exchange stream, overlapping the next step).
         CPU tensors: synchronous."""
+        direct = self._direct(B_full) if B_full is not None and not self.host_gather else None
+        if direct is not None and self.world == 1 and (self.cuda or not self.dist):
+            self._step_in_place(direct)
+            return
         slot = self.steps % self.SLOTS
         self.steps += 1
         main = torch.cuda.current_stream(self.xs.device) if self.cuda else None
@@ -125,12 +149,13 @@ class _Pipeline:
         for c, (j0, j1) in enumerate(self.cols):
             self._compute(c, j0, j1, self.local[slot][c])
             if self.host_gather and B_full is not None:   # synchronous, through host memory
-                out = torch.empty(self.gathered[slot][c].shape, dtype=self.local[slot][c].dtype)
+                out = torch.empty(self.gathered(slot, c).shape, dtype=self.local[slot][c].dtype)
                 dist.all_gather_into_tensor(out, self.local[slot][c].cpu(), group=self.group)
-                self.gathered[slot][c].copy_(out)
+                self.gathered(slot, c).copy_(out)
             elif self.dist and B_full is not None:   # issued behind this chunk's compute
-                works.append(dist.all_gather_into_tensor(self.gathered[slot][c], self.local[slot][c],
-                                                         group=self.group, async_op=True))
+                dst = direct if direct is not None else self.gathered(slot, c)
+                works.append(dist.all_gather_into_tensor(dst, self.local[slot][c], group=self.group,
+                                                         async_op=True))
         if self.cuda and self.timing:
             self.marks[-1].append(self._ev(main))
         if B_full is None:
@@ -139,21 +164,50 @@ class _Pipeline:
             for c, (j0, j1) in enumerate(self.cols):
                 if self.dist:
                     works[c].wait()
-                self._unpack_chunk(c, j0, j1, self.gathered[slot][c] if self.dist else self.local[slot][c], B_full)
+                if direct is None or not self.dist:
+                    self._unpack_chunk(c, j0, j1, self.gathered(slot, c) if self.dist else self.local[slot][c],
+                                       B_full)
             return
         self.xs.wait_stream(main)   # the shards (and B_full's previous users) are done
         with torch.cuda.stream(self.xs):
             for c, (j0, j1) in enumerate(self.cols):
                 if works:
                     works[c].wait()   # this stream waits for the collective
-                src = self.gathered[slot][c] if self.dist else self.local[slot][c]
-                self._unpack_chunk(c, j0, j1, src, B_full)
+                if direct is None or not self.dist:   # (a direct gather wrote B_full itself)
+                    src = self.gathered(slot, c) if self.dist else self.local[slot][c]
+                    self._unpack_chunk(c, j0, j1, src, B_full)
             ev = torch.cuda.Event()
             ev.record(self.xs)
         self.slot_free[slot] = ev
 
+    def _step_in_place(self, out: torch.Tensor) -> None:
+        """One rank, one chunk: the shard is the whole sketch. Compute straight into B_full and
+        all-gather in place (RCCL's in-place form, input = the rank's block of the output: no
+        copy), so the step moves no bytes beyond the compute's own. The next step's compute waits
+        for this gather (it reads B_full)."""
+        main = torch.cuda.current_stream(self.xs.device) if self.cuda else None
+        if self.pending is not None:
+            self.pending.wait()   # the previous in-place gather (CUDA: a stream wait, not a host one)
+        if self.cuda:
+            for ev in self.slot_free:   # exchanges of earlier pipelined steps into this B_full
+                if ev is not None:
+                    main.wait_event(ev)
+            self.slot_free = [None] * self.SLOTS
+        if self.cuda and self.timing:
+            self.marks.append([self._ev(main)])
+        j0, j1 = self.cols[0]
+        self._compute(0, j0, j1, out)
+        if self.cuda and self.timing:
+            self.marks[-1].append(self._ev(main))
+        self.pending = (dist.all_gather_into_tensor(out, out, group=self.group, async_op=True)
+                        if self.dist else None)
+        self.steps += 1
+
     def wait(self) -> None:
         """Make the caller's current stream wait for every enqueued exchange (B_full complete)."""
+        if self.pending is not None:
+            self.pending.wait()
+            self.pending = None
         if self.cuda:
             torch.cuda.current_stream(self.xs.device).wait_stream(self.xs)
 
@@ -186,6 +240,12 @@ class RowShardedSketch(_Pipeline):
     def _compute(self, c, j0, j1, out):
         self.compute(self.ro_s, j0, j1, out)
 
+    def _direct(self, B_full):
+        # one rank holds every row: its (single-chunk) shard is B itself
+        if self.world == 1 and len(self.cols) == 1:
+            return B_full[:self.d_total * self.n]
+        return None
+
     def _unpack_chunk(self, c, j0, j1, src, B_full):
         # ColMajor d_total x n: column j of rank g's shard lands at j * d_total + g * d_loc
         _unpack(src, self.world, j1 - j0, self.d_loc, B_full[j0 * self.d_total:], self.d_total, self.d_loc)
@@ -209,6 +269,12 @@ class ColumnShardedSketch(_Pipeline):
 
     def _compute(self, c, j0, j1, out):
         self.compute(j0, j1, out)
+
+    def _direct(self, B_full):
+        # ColMajor: rank g's d x n_loc block is contiguous at g n_loc d, the all-gather's own order
+        if len(self.cols) == 1:
+            return B_full[:self.world * self.n_loc * self.d]
+        return None
 
     def _unpack_chunk(self, c, j0, j1, src, B_full):
         # [rank][local column][row]: rank g's column j0 + j at (g n_loc + j0 + j) d

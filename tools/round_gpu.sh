@@ -8,8 +8,8 @@ cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 what="${*:-tests bench prof pmc}"
-CONFIGS="${CONFIGS:-c2 ns c3 c4 c5}"
-PMC_CONFIGS="${PMC_CONFIGS:-c2 c3}"
+CONFIGS="${CONFIGS:-c2 c1 ns c3 c4 c5 c5p}"
+PMC_CONFIGS="${PMC_CONFIGS:-c2 c3 c4}"
 
 run() {   # run <log> <timeout> <cmd...>
     local logf="$1" tmo="$2"; shift 2
@@ -27,6 +27,10 @@ case " $what " in *" tests "*)
 ;; esac
 case " $what " in *" bench "*)
     for c in $CONFIGS; do run "bench_$c.log" 300 python -u bench.py --config "$c"; done
+    run bench_c3pre.log 300 python -u bench.py --config c3 --prefilled
+    for c in ${DIST_CONFIGS:-c2 ns c3 c4}; do
+        run "bench_${c}_dist1.log" 300 python -u bench.py --config "$c" --dist --no-cpu-baseline
+    done
 ;; esac
 case " $what " in *" prof "*)
     for c in $CONFIGS; do
