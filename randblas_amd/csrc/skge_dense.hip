@@ -1176,13 +1176,13 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
 //    round, so the draw is spread evenly over the four SIMDs and the waves meet once per round.
 // Requires K % (128 / sizeof(T)) == 0, a memory operand with 16-B aligned rows contiguous along k
 // (mode 2), pc0 % 4 == 0, and the wave's 128 rows addressable with 32-bit byte offsets.
-template <typename T, int GK, int FAMILY, bool GX, bool SPLIT, int PF, int BG>
+template <typename T, int GK, int FAMILY, bool GX, bool SPLIT, int PF, int BG, int MW>
 __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     constexpr int KS = 128 / (int)sizeof(T);              // k per step
     constexpr int VPL = 32 / (int)sizeof(T);              // k values per lane and step: k = VPL g + v
     constexpr int EPS = 16 / (int)sizeof(T);              // elements per 16-B slot
-    constexpr int BMW = 128;                              // memory rows per wave
-    constexpr int FA = BG / 16, FB = BMW / 16;            // FA x 8 MFMA tiles per wave
+    constexpr int BMW = MW;                               // memory rows per wave (128; f64 64)
+    constexpr int FA = BG / 16, FB = BMW / 16;            // FA x FB MFMA tiles per wave
     constexpr int R = 4;                                  // steps per round
     constexpr int SLOT_B = BG * 128;                      // bytes per generated tile (BG rows x 128 B)
     constexpr int CPS = BG * KS / 4;                      // Philox calls per step (f64 128, f32 512)
@@ -1666,7 +1666,8 @@ static bool wide_ok(const GemmProblem &p) {
 // workgroup), BG = 64 work priced at 0.93 of BG = 32's per row (that measurement). C4 (d = 256,
 // 128 tiles of 64 x 1024) takes BG = 64 with split 2 (256 workgroups).
 struct StreamGeom {
-    int bg;
+    int bg;      // generated rows per tile
+    int mw;      // memory rows per wave (the tile's memory rows: 8 mw)
     int split;
 };
 constexpr double STREAM_BG64_COST = 0.93;
@@ -1677,13 +1678,14 @@ static StreamGeom stream_geom(const GemmProblem &p) {
     const int64_t nk = p.K / BK;   // 16-deep steps, as the 64 x 512 kernels count them
     const int64_t wide = ((gnO + 63) / 64) * ((mnO + 511) / 512);
     const int s32 = choose_split(wide, nk, p.split_req);
-    if (sizeof(T) == 8 || RBH_STREAM_BG32 != 64) return {32, s32};
+    if (sizeof(T) == 8) return {64, 64, s32};   // the wide kernel's 64 x 512 tiles
+    if (RBH_STREAM_BG32 != 64) return {32, 128, s32};
     const int64_t t64 = ((gnO + 63) / 64) * ((mnO + 1023) / 1024), t32 = ((gnO + 31) / 32) * ((mnO + 1023) / 1024);
     const int s64 = choose_split(t64, nk, p.split_req);
     const int64_t cus = device_cus();
     const double c32 = (double)((t32 * s32 + cus - 1) / cus) * 32.0 / s32;
     const double c64 = (double)((t64 * s64 + cus - 1) / cus) * 64.0 * STREAM_BG64_COST / s64;
-    return c64 < c32 ? StreamGeom{64, s64} : StreamGeom{32, s32};
+    return c64 < c32 ? StreamGeom{64, 128, s64} : StreamGeom{32, 128, s32};
 }
 
 template <int GK, int FAMILY, bool GX>
@@ -1769,7 +1771,7 @@ template <typename T, int GK, int FAMILY, bool GX>
 static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
     const int64_t gnO = GX ? p.M : p.N, mnO = GX ? p.N : p.M;
     const StreamGeom gm = stream_geom<T>(p);
-    const int64_t nb = ((gnO + gm.bg - 1) / gm.bg) * ((mnO + 1023) / 1024);
+    const int64_t nb = ((gnO + gm.bg - 1) / gm.bg) * ((mnO + 8 * gm.mw - 1) / (8 * gm.mw));
     if (nb <= 0) return hipSuccess;
     const int split = gm.split;
     GemmProblem q = p;
@@ -1782,13 +1784,16 @@ static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
     }
     timing_begin(s);
     const dim3 grid((unsigned)(nb * split));
-    constexpr int BGW = sizeof(T) == 4 ? 64 : 32;   // (f64 never takes BG = 64: 256 accumulator registers)
-    if (gm.bg == 64) {
-        if (split > 1) hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, stream_pf<T>(), BGW>), grid, dim3(512), 0, s, q);
-        else hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, stream_pf<T>(), BGW>), grid, dim3(512), 0, s, q);
+    constexpr int PF = stream_pf<T>();
+    if constexpr (sizeof(T) == 8) {   // 64 x 512 tiles (64 x 1024 would take 256 accumulator registers)
+        if (split > 1) hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, PF, 64, 64>), grid, dim3(512), 0, s, q);
+        else hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, PF, 64, 64>), grid, dim3(512), 0, s, q);
+    } else if (gm.bg == 64) {
+        if (split > 1) hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, PF, 64, 128>), grid, dim3(512), 0, s, q);
+        else hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, PF, 64, 128>), grid, dim3(512), 0, s, q);
     } else {
-        if (split > 1) hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, stream_pf<T>(), 32>), grid, dim3(512), 0, s, q);
-        else hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, stream_pf<T>(), 32>), grid, dim3(512), 0, s, q);
+        if (split > 1) hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, PF, 32, 128>), grid, dim3(512), 0, s, q);
+        else hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, PF, 32, 128>), grid, dim3(512), 0, s, q);
     }
     e = hipGetLastError();
     if (split > 1 && e == hipSuccess) {
@@ -1878,7 +1883,7 @@ static GemmPlan plan_gemm(const GemmProblem &p) {
         const int64_t gnO = gx ? p.M : p.N, mnO = gx ? p.N : p.M;
         const StreamGeom gm = stream_geom<T>(p);   // as launch_stream
         pl.kernel = PLAN_STREAM;
-        pl.tiles = ((gnO + gm.bg - 1) / gm.bg) * ((mnO + 1023) / 1024);
+        pl.tiles = ((gnO + gm.bg - 1) / gm.bg) * ((mnO + 8 * gm.mw - 1) / (8 * gm.mw));
         pl.splitk = gm.split;
     } else if (wide_ok<T>(p)) {
         pl.kernel = PLAN_WIDE;
