@@ -159,10 +159,22 @@ def relaunch(ngpus: int) -> int:
     import socket
     import subprocess
 
-    sk = socket.socket()
-    sk.bind(("127.0.0.1", 0))
-    port = sk.getsockname()[1]
-    sk.close()
+    import random
+
+    port = None   # below the ephemeral range, so no outgoing connection takes it before torchrun binds it
+    for _ in range(200):
+        cand = random.SystemRandom().randrange(20000, 32000)
+        sk = socket.socket()
+        try:
+            sk.bind(("127.0.0.1", cand))
+            port = cand
+            break
+        except OSError:
+            continue
+        finally:
+            sk.close()
+    if port is None:
+        raise SystemExit("bench: no free rendezvous port in 20000-32000")
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ngpus}",

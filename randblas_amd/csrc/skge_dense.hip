@@ -1176,7 +1176,10 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
 //    round, so the draw is spread evenly over the four SIMDs and the waves meet once per round.
 // Requires K % (128 / sizeof(T)) == 0, a memory operand with 16-B aligned rows contiguous along k
 // (mode 2), pc0 % 4 == 0, and the wave's 128 rows addressable with 32-bit byte offsets.
-template <typename T, int GK, int FAMILY, bool GX, bool SPLIT, int PF, int BG, int MW>
+#ifndef RBH_STREAM_PARTS64
+#define RBH_STREAM_PARTS64 2   // f64 64 x 512: a step in two 16-B parts (variant builds: 1)
+#endif
+template <typename T, int GK, int FAMILY, bool GX, bool SPLIT, int PF, int BG, int MW, int TRI = 0>
 __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     constexpr int KS = 128 / (int)sizeof(T);              // k per step
     constexpr int VPL = 32 / (int)sizeof(T);              // k values per lane and step: k = VPL g + v
@@ -1190,7 +1193,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     constexpr int WCALLS = R / SPU;                       // wave-calls per wave and round (f64 1, f32 4)
     // a step runs in NPART parts: BG = 64 in two (each the lane's next 16 B: half the fragment
     // registers, for the 128 accumulators), BG = 32 in one (the lane's 32 B)
-    constexpr int NPART = BG == 64 ? 2 : 1;
+    constexpr int NPART = BG == 64 ? (sizeof(T) == 8 ? RBH_STREAM_PARTS64 : 2) : 1;
     constexpr int PV = VPL / NPART;                       // values per lane and part
     constexpr int NLD = 2 / NPART;                        // 16-B loads per part fragment
     constexpr int NH = NPART * FB;                        // part-blocks of a step (part FB + c)
@@ -1229,30 +1232,88 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     // the step's 128-B window, through a buffer resource based at the wave's first row (rows past
     // the operand clamped to its last row; their outputs are discarded)
     const T *mptr = (const T *)mop.ptr;
-    const int64_t wbase = wm0 < mnO ? wm0 : mnO - 1;
+    const int64_t wbase = TRI ? 0 : (wm0 < mnO ? wm0 : mnO - 1);
     const __amdgpu_buffer_rsrc_t mrsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)(mptr + wbase * mop.so), (short)0, -1, 0x00020000);
+    // One-triangle operand (TRI 1-4, as skge_wide_kernel): element (o, k) is stored at rowbase(o) + k
+    // inside the triangle and is the stored (k, o) outside; the resource is based at the matrix and
+    // the launcher checks that every byte offset of the stored triangle fits in 32 bits.
+    constexpr bool TKLE = TRI == 1 || TRI == 3;
+    const uint32_t tso = (uint32_t)mop.so, tn = (uint32_t)p.tri_n;
+    auto rowbase = [&](uint32_t a) -> uint32_t {
+        if (TRI == 3) return a * (a + 1) / 2;
+        if (TRI == 4) return a * tn - a * (a + 1) / 2;
+        return a * tso;
+    };
     uint32_t voff[FB];
 #pragma unroll
     for (int c = 0; c < FB; ++c) {
         int64_t row = wm0 + 16 * c + r;
         row = row < mnO ? row : mnO - 1;
-        voff[c] = (uint32_t)(((row - wbase) * mop.so + (int64_t)VPL * g) * (int64_t)sizeof(T));
+        voff[c] = TRI ? (uint32_t)((rowbase((uint32_t)row) + VPL * g) * sizeof(T))
+                      : (uint32_t)(((row - wbase) * mop.so + (int64_t)VPL * g) * (int64_t)sizeof(T));
     }
+    // Mirrored steps read the lane's element (o, K0 + a + j), a = VPL g, as the stored (s + a, o) with
+    // s = K0 + j: rowbase(s + a) + o = rowbase(s) [uniform, soffset] + a so + o (full storage),
+    // + s a + a (a + 1) / 2 + o (packed lower), or + a n - s a - a (a + 1) / 2 + o (packed upper):
+    // a per-lane constant vmir[c] plus at most one multiply-add by the uniform s.
+    const uint32_t a8 = (uint32_t)(VPL * g * sizeof(T));
+    uint32_t vmir[TRI ? FB : 1];
+    if (TRI) {
+#pragma unroll
+        for (int c = 0; c < FB; ++c) {
+            int64_t row = wm0 + 16 * c + r;
+            row = row < mnO ? row : mnO - 1;
+            const uint32_t a = VPL * g, t0 = a * (a + 1) / 2;
+            const uint32_t lane_part = TRI <= 2 ? a * tso : (TRI == 3 ? t0 : a * tn - t0);
+            vmir[c] = (uint32_t)((lane_part + (uint32_t)row) * sizeof(T));
+        }
+    }
+    // the step's class for this wave (uniform): 0 inside the triangle, 1 mirrored, 2 straddles the
+    // diagonal. The wave's rows (clamped) lie in [rlo, rhi].
+    const int rlo = (int)(wm0 < mnO ? wm0 : mnO - 1), rhi = (int)(wm0 + BMW - 1 < mnO ? wm0 + BMW - 1 : mnO - 1);
+    auto tclass = [&](int64_t kt) -> int {
+        const int K0 = (int)(kt * KS);
+        if (TKLE) return K0 + KS - 1 <= rlo ? 0 : (K0 > rhi ? 1 : 2);
+        return K0 >= rhi ? 0 : (K0 + KS - 1 < rlo ? 1 : 2);
+    };
     // part p contracts the lane's values v = PV p .. PV p + PV - 1 (its 16-B slots 2 g + NLD p + l,
     // l < NLD); the ring holds part-blocks
     hv_t mv[NSLOT];
     auto mload = [&](int slot, int i, int64_t kt) {   // part-block i = p FB + c of step kt
         const uint32_t soff = (uint32_t)(kt * 128);
-        pf_t x;
+        const int cls = TRI ? tclass(kt) : 0;
+        if (cls == 0) {
+            pf_t x;
 #pragma unroll
-        for (int l = 0; l < NLD; ++l) {
-            const v4f y = __builtin_bit_cast(
-                v4f, __builtin_amdgcn_raw_buffer_load_b128(mrsrc, voff[i % FB] + 16u * (NLD * (i / FB) + l), soff, 0));
+            for (int l = 0; l < NLD; ++l) {
+                const v4f y = __builtin_bit_cast(
+                    v4f, __builtin_amdgcn_raw_buffer_load_b128(mrsrc, voff[i % FB] + 16u * (NLD * (i / FB) + l), soff, 0));
 #pragma unroll
-            for (int e = 0; e < 4; ++e) x[4 * l + e] = y[e];
+                for (int e = 0; e < 4; ++e) x[4 * l + e] = y[e];
+            }
+            mv[slot] = __builtin_bit_cast(hv_t, x);
+            return;
         }
-        mv[slot] = __builtin_bit_cast(hv_t, x);
+        const int c = i % FB;
+        const uint32_t K0 = (uint32_t)(kt * KS);
+#pragma unroll
+        for (int e = 0; e < PV; ++e) {
+            const uint32_t j = (uint32_t)(PV * (i / FB) + e), sk = K0 + j;
+            uint32_t vo = vmir[c];
+            if (TRI == 3) vo += sk * a8;
+            if (TRI == 4) vo -= sk * a8;
+            uint32_t so_ = rowbase(sk) * (uint32_t)sizeof(T);
+            if (cls == 2) {   // per element: inside (rowbase(o) + k) or mirrored
+                int64_t row = wm0 + 16 * c + r;
+                row = row < mnO ? row : mnO - 1;
+                const uint32_t k = sk + VPL * g;
+                const bool in = TKLE ? k <= (uint32_t)row : k >= (uint32_t)row;
+                vo = in ? voff[c] + sk * (uint32_t)sizeof(T) : vo + so_;
+                so_ = 0;
+            }
+            mv[slot][e] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(mrsrc, vo, so_, 0));
+        }
     };
 
     // ---- generated operand: slot (ring half, step t) holds rows o < 32 of 8 16-B slots each, slot q
@@ -1742,12 +1803,11 @@ static bool wide32_ok(const GemmProblem &p) {
 
 // The streamed wide kernel takes every wide-kernel problem whose operator is drawn in the GEMM (a
 // materialised window keeps the 64 x 512 GMAT kernels): same conditions, bitwise the same sums.
-// f64 stays on the 64 x 512 kernel: measured C2 8.72 ms there against 8.92-9.15 ms streamed (PF 1,
-// 3, 7; same box, two alternations). The f64 MFMA is twice as long, so halving the draws saves half
-// as much per MFMA, while the streamed tile doubles the memory loads per MFMA. f32 (C4): 4.71 ms
-// streamed against 4.90-4.94 ms on skge_wide32_kernel.
+// f64 streams the wide kernel's own 64 x 512 tiles (C2: 7.99-8.01 ms against 8.72-8.74 ms on
+// skge_wide_kernel, same box, two alternations); f32 streams 64 or 32 x 1024 tiles (stream_geom).
+// The macros exist for variant builds (A/B timing): 0 keeps that type on the 64 x 512 LDS kernels.
 #ifndef RBH_STREAM64
-#define RBH_STREAM64 0   // (variant builds for A/B timing: 1 puts f64 on the streamed kernel)
+#define RBH_STREAM64 1
 #endif
 #ifndef RBH_STREAM32
 #define RBH_STREAM32 1
@@ -1760,14 +1820,14 @@ static bool stream_ok(const GemmProblem &p) {
 
 // part-blocks loaded ahead of their use (a register ring of PF + 1; PF + 1 divides 8)
 #ifndef RBH_STREAM_PF64
-#define RBH_STREAM_PF64 3
+#define RBH_STREAM_PF64 7   // (C2: PF 7 7.99-8.01 ms, PF 3 8.15-8.19 ms)
 #endif
 #ifndef RBH_STREAM_PF32
 #define RBH_STREAM_PF32 3
 #endif
 template <typename T> constexpr int stream_pf() { return sizeof(T) == 8 ? RBH_STREAM_PF64 : RBH_STREAM_PF32; }
 
-template <typename T, int GK, int FAMILY, bool GX>
+template <typename T, int GK, int FAMILY, bool GX, int TRI = 0>
 static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
     const int64_t gnO = GX ? p.M : p.N, mnO = GX ? p.N : p.M;
     const StreamGeom gm = stream_geom<T>(p);
@@ -1784,10 +1844,10 @@ static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
     }
     timing_begin(s);
     const dim3 grid((unsigned)(nb * split));
-    constexpr int PF = stream_pf<T>();
+    constexpr int PF = TRI ? 3 : stream_pf<T>();   // (the one-triangle loads need 5 more registers)
     if constexpr (sizeof(T) == 8) {   // 64 x 512 tiles (64 x 1024 would take 256 accumulator registers)
-        if (split > 1) hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, PF, 64, 64>), grid, dim3(512), 0, s, q);
-        else hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, PF, 64, 64>), grid, dim3(512), 0, s, q);
+        if (split > 1) hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, PF, 64, 64, TRI>), grid, dim3(512), 0, s, q);
+        else hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, PF, 64, 64, TRI>), grid, dim3(512), 0, s, q);
     } else if (gm.bg == 64) {
         if (split > 1) hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, PF, 64, 128>), grid, dim3(512), 0, s, q);
         else hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, PF, 64, 128>), grid, dim3(512), 0, s, q);
@@ -1809,9 +1869,19 @@ static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
     return e;
 }
 
-// the wide kernel instantiated for one-triangle operand p.tri (1-4)
+// the wide kernel instantiated for one-triangle operand p.tri (1-4): streamed (the default) or
+// through LDS (a materialised window, or RBH_STREAM64=0 builds)
 template <int FAM, bool GX>
 static hipError_t launch_wide_tri(const GemmProblem &p, hipStream_t s) {
+    if (RBH_STREAM64 && !p.materialise) {
+        switch (p.tri) {
+        case 1: return launch_stream<double, GEN_OK, FAM, GX, 1>(p, s);
+        case 2: return launch_stream<double, GEN_OK, FAM, GX, 2>(p, s);
+        case 3: return launch_stream<double, GEN_OK, FAM, GX, 3>(p, s);
+        case 4: return launch_stream<double, GEN_OK, FAM, GX, 4>(p, s);
+        }
+        return hipErrorInvalidValue;
+    }
     switch (p.tri) {
     case 1: return launch_wide<GEN_OK, FAM, GX, 1>(p, s);
     case 2: return launch_wide<GEN_OK, FAM, GX, 2>(p, s);

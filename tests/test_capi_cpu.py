@@ -122,8 +122,8 @@ def _plan(d, n, m, D_rows=None, ro=0, dtype="f64", opts=None, layout="C"):
 
 
 def test_plan_baseline_configs():
-    # C2 (512 wide tiles): a full grid, no split
-    assert _plan(1024, 16384, 16384) == rb.Plan("wide", 1, 512, 512)
+    # C2 (512 streamed 64 x 512 tiles): a full grid, no split
+    assert _plan(1024, 16384, 16384) == rb.Plan("stream", 1, 512, 512)
     # C4 per GPU: 128 streamed 64 x 1024 tiles, split 2 (priced below 256 unsplit 32 x 1024 tiles)
     assert _plan(256, 32768, 32768, D_rows=2048, ro=1792, dtype="f32") == rb.Plan("stream", 2, 128, 256)
     # f32 at C2's shape: 256 tiles of 64 x 1024 fill the chip once (32 x 1024 would take two waves)
@@ -131,9 +131,9 @@ def test_plan_baseline_configs():
     # too little K to split: 256 tiles of 32 x 1024 beat 128 of 64 x 1024
     assert _plan(256, 32768, 1024, dtype="f32") == rb.Plan("stream", 1, 256, 256)
     # C1: 16 tiles -> 16 slices of K = 4096
-    assert _plan(128, 4096, 4096) == rb.Plan("wide", 16, 16, 256)
+    assert _plan(128, 4096, 4096) == rb.Plan("stream", 16, 16, 256)
     # the north star split over 8 ranks: 128 tiles fill half the chip -> split 2
-    assert _plan(256, 16384, 16384, D_rows=2048, ro=1792) == rb.Plan("wide", 2, 128, 256)
+    assert _plan(256, 16384, 16384, D_rows=2048, ro=1792) == rb.Plan("stream", 2, 128, 256)
     # a quarter of C4's rank columns alone would split 8: the sharded driver passes the whole split
     assert _plan(256, 8192, 32768, D_rows=2048, ro=1792, dtype="f32") == rb.Plan("stream", 8, 32, 256)
     assert _plan(256, 8192, 32768, D_rows=2048, ro=1792, dtype="f32",
@@ -144,7 +144,7 @@ def test_plan_baseline_configs():
 
 def test_plan_options_fix_the_split():
     assert _plan(128, 4096, 4096, opts=rb.Options(splitk=1)).splitk == 1
-    assert _plan(128, 4096, 4096, opts=rb.Options(splitk=3)) == rb.Plan("wide", 3, 16, 48)
+    assert _plan(128, 4096, 4096, opts=rb.Options(splitk=3)) == rb.Plan("stream", 3, 16, 48)
     assert _plan(1024, 16384, 16384, opts=rb.Options(splitk=2)).splitk == 2
     # RowMajor A with lda = n is contiguous along the output columns, not along the contracted
     # index: the generic kernel (scalar loads along the outer index)

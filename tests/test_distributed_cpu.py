@@ -4,21 +4,18 @@ Each rank computes its ro_s-offset row shard with the CPU oracle, the shards are
 unpacked; the reassembled sketch must equal the unsharded oracle sketch (bitwise for SASO, whose
 accumulation order is fixed; to BLAS rounding for the dense product)."""
 import os
-import socket
 
 import numpy as np
 import pytest
+
+from ports import free_port
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    return free_port()
 
 
 def _worker(rank, world, port, kind, chunks, q):

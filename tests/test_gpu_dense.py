@@ -316,7 +316,7 @@ def test_materialised_equals_drawn_bitwise(cuda, dtype):
 # 4096: 16 output tiles at K = 4096 -> automatic split 16; forced 1 (unsplit) and 3 (uneven
 # slices). RowMajor with opA = T keeps A contiguous along the contracted index (the wide kernels'
 # memory operand). Within E of the oracle; the plan names the kernel that ran.
-@pytest.mark.parametrize("dtype,kernel", [(np.float32, "stream"), (np.float64, "wide")])
+@pytest.mark.parametrize("dtype,kernel", [(np.float32, "stream"), (np.float64, "stream")])
 @pytest.mark.parametrize("layout,opA", [("C", "N"), ("R", "T")])
 @pytest.mark.parametrize("split", [0, 1, 3])
 def test_wide_split_k_within_bound(cuda, dtype, kernel, layout, opA, split):
@@ -326,7 +326,9 @@ def test_wide_split_k_within_bound(cuda, dtype, kernel, layout, opA, split):
     lda = m
     plan = rb.plan_left(layout, "N", opA, d, n, m, S, 256, lda, d if layout == "C" else n, ro_s=4,
                         dtype="f64" if dtype == np.float64 else "f32", options=opts)
-    assert plan.kernel == kernel and plan.splitk == (16 if split == 0 else split), plan
+    # (f64 builds without the streamed kernel run the 64 x 512 LDS kernel: the same tiles and sums)
+    assert plan.kernel in ((kernel, "wide") if dtype == np.float64 else (kernel,)), plan
+    assert plan.splitk == (16 if split == 0 else split), plan
     check_left(cuda, layout, "N", opA, d, n, m, 1.0, -0.5, d + 4, m, 4, 0, dtype, options=opts)
 
 

@@ -4,21 +4,18 @@ every rank, bitwise against single calls (tests/multirank_worker.py). RCCL canno
 one GPU, so the N-rank RCCL runs stay the driver's 8-GPU node; this is the multi-rank HIP check
 that fits one card. Each launcher is a child process."""
 import os
-import socket
 import subprocess
 import sys
 
 import pytest
 
+from ports import free_port
+
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    return free_port()
 
 
 @pytest.mark.gpu

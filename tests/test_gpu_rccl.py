@@ -4,21 +4,18 @@ path -- all_gather_into_tensor over RCCL, then the HIP unpack (randblas_amd/dist
 bench.py --dist times that step. Each launcher is a child process (never an exec)."""
 import json
 import os
-import socket
 import subprocess
 import sys
 
 import pytest
 
+from ports import free_port
+
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    return free_port()
 
 
 def _torchrun(args, timeout=110):
