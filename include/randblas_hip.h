@@ -164,7 +164,8 @@ typedef struct rbh_options {
 
 /* The kernel a dense sketch call would launch: kernel 0 none (empty output), 1 beta-scaling only,
  * 2 generic GEMM, 3 fused GEMM, 4 wide f64 GEMM, 5 wide f32 GEMM (32-deep), 6 wide one-triangle
- * GEMM, 7 triangle expanded, then the plain kernels; its output tiles, split-K factor and
+ * GEMM, 7 triangle expanded, then the plain kernels, 8 streamed GEMM (the default for the wide
+ * kernels' problems), 9 streamed one-triangle GEMM; its output tiles, split-K factor and
  * workgroups (tiles * splitk). */
 typedef struct rbh_plan {
     int32_t kernel;

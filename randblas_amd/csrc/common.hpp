@@ -73,7 +73,8 @@ enum PlanKernel : int {
     PLAN_WIDE32 = 5,      // skge_wide32_kernel (f32)
     PLAN_WIDE_TRI = 6,    // skge_wide_kernel with a one-triangle symmetric operand
     PLAN_SYMMETRIZE = 7,  // one-triangle operand expanded into a workspace, then the plain kernels
-    PLAN_STREAM = 8,      // skge_stream_kernel (the wide kernels' sums; 32 or 64 x 1024 tiles)
+    PLAN_STREAM = 8,      // skge_stream_kernel (the wide kernels' sums; f64 64 x 512, f32 32 / 64 x 1024)
+    PLAN_STREAM_TRI = 9,  // skge_stream_kernel with a one-triangle symmetric operand (f64)
 };
 struct GemmPlan {
     int kernel;

@@ -1282,38 +1282,40 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     hv_t mv[NSLOT];
     auto mload = [&](int slot, int i, int64_t kt) {   // part-block i = p FB + c of step kt
         const uint32_t soff = (uint32_t)(kt * 128);
-        const int cls = TRI ? tclass(kt) : 0;
-        if (cls == 0) {
-            pf_t x;
+        if constexpr (TRI != 0) {
+            const int cls = tclass(kt);
+            if (cls != 0) {   // mirrored or straddling: one 8-B load per element
+                const int c = i % FB;
+                const uint32_t K0 = (uint32_t)(kt * KS);
 #pragma unroll
-            for (int l = 0; l < NLD; ++l) {
-                const v4f y = __builtin_bit_cast(
-                    v4f, __builtin_amdgcn_raw_buffer_load_b128(mrsrc, voff[i % FB] + 16u * (NLD * (i / FB) + l), soff, 0));
-#pragma unroll
-                for (int e = 0; e < 4; ++e) x[4 * l + e] = y[e];
+                for (int e = 0; e < PV; ++e) {
+                    const uint32_t j = (uint32_t)(PV * (i / FB) + e), sk = K0 + j;
+                    uint32_t vo = vmir[c];
+                    if (TRI == 3) vo += sk * a8;
+                    if (TRI == 4) vo -= sk * a8;
+                    uint32_t so_ = rowbase(sk) * (uint32_t)sizeof(T);
+                    if (cls == 2) {   // per element: inside (rowbase(o) + k) or mirrored
+                        int64_t row = wm0 + 16 * c + r;
+                        row = row < mnO ? row : mnO - 1;
+                        const uint32_t k = sk + VPL * g;
+                        const bool in = TKLE ? k <= (uint32_t)row : k >= (uint32_t)row;
+                        vo = in ? voff[c] + sk * (uint32_t)sizeof(T) : vo + so_;
+                        so_ = 0;
+                    }
+                    mv[slot][e] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(mrsrc, vo, so_, 0));
+                }
+                return;
             }
-            mv[slot] = __builtin_bit_cast(hv_t, x);
-            return;
         }
-        const int c = i % FB;
-        const uint32_t K0 = (uint32_t)(kt * KS);
+        pf_t x;
 #pragma unroll
-        for (int e = 0; e < PV; ++e) {
-            const uint32_t j = (uint32_t)(PV * (i / FB) + e), sk = K0 + j;
-            uint32_t vo = vmir[c];
-            if (TRI == 3) vo += sk * a8;
-            if (TRI == 4) vo -= sk * a8;
-            uint32_t so_ = rowbase(sk) * (uint32_t)sizeof(T);
-            if (cls == 2) {   // per element: inside (rowbase(o) + k) or mirrored
-                int64_t row = wm0 + 16 * c + r;
-                row = row < mnO ? row : mnO - 1;
-                const uint32_t k = sk + VPL * g;
-                const bool in = TKLE ? k <= (uint32_t)row : k >= (uint32_t)row;
-                vo = in ? voff[c] + sk * (uint32_t)sizeof(T) : vo + so_;
-                so_ = 0;
-            }
-            mv[slot][e] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(mrsrc, vo, so_, 0));
+        for (int l = 0; l < NLD; ++l) {
+            const v4f y = __builtin_bit_cast(
+                v4f, __builtin_amdgcn_raw_buffer_load_b128(mrsrc, voff[i % FB] + 16u * (NLD * (i / FB) + l), soff, 0));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[4 * l + e] = y[e];
         }
+        mv[slot] = __builtin_bit_cast(hv_t, x);
     };
 
     // ---- generated operand: slot (ring half, step t) holds rows o < 32 of 8 16-B slots each, slot q
@@ -1826,6 +1828,9 @@ static bool stream_ok(const GemmProblem &p) {
 #define RBH_STREAM_PF32 3
 #endif
 template <typename T> constexpr int stream_pf() { return sizeof(T) == 8 ? RBH_STREAM_PF64 : RBH_STREAM_PF32; }
+#ifndef RBH_STREAM_PF_TRI
+#define RBH_STREAM_PF_TRI 7   // the one-triangle (f64) instantiations
+#endif
 
 template <typename T, int GK, int FAMILY, bool GX, int TRI = 0>
 static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
@@ -1844,7 +1849,7 @@ static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
     }
     timing_begin(s);
     const dim3 grid((unsigned)(nb * split));
-    constexpr int PF = TRI ? 3 : stream_pf<T>();   // (the one-triangle loads need 5 more registers)
+    constexpr int PF = TRI ? RBH_STREAM_PF_TRI : stream_pf<T>();
     if constexpr (sizeof(T) == 8) {   // 64 x 512 tiles (64 x 1024 would take 256 accumulator registers)
         if (split > 1) hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, PF, 64, 64, TRI>), grid, dim3(512), 0, s, q);
         else hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, PF, 64, 64, TRI>), grid, dim3(512), 0, s, q);
@@ -1869,11 +1874,17 @@ static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
     return e;
 }
 
-// the wide kernel instantiated for one-triangle operand p.tri (1-4): streamed (the default) or
-// through LDS (a materialised window, or RBH_STREAM64=0 builds)
+// The one-triangle operand stays on skge_wide_kernel by default: streamed, each mirrored step
+// loads 8 B per element (the stored row k holds the lane's row o at a 16-row stride), and C5p
+// measured 4.85 ms against 4.59-4.61 ms through the wide kernel's LDS transpose (same box, two
+// alternations; with PF 3 5.27-5.30 ms). RBH_STREAM_TRI=1 builds stream it (variant A/B timing).
+#ifndef RBH_STREAM_TRI
+#define RBH_STREAM_TRI 0
+#endif
+// the wide kernel instantiated for one-triangle operand p.tri (1-4): through LDS, or streamed
 template <int FAM, bool GX>
 static hipError_t launch_wide_tri(const GemmProblem &p, hipStream_t s) {
-    if (RBH_STREAM64 && !p.materialise) {
+    if (RBH_STREAM_TRI && RBH_STREAM64 && !p.materialise) {
         switch (p.tri) {
         case 1: return launch_stream<double, GEN_OK, FAM, GX, 1>(p, s);
         case 2: return launch_stream<double, GEN_OK, FAM, GX, 2>(p, s);
@@ -1945,7 +1956,7 @@ static GemmPlan plan_gemm(const GemmProblem &p) {
         return pl;
     }
     if (p.tri) {
-        pl.kernel = PLAN_WIDE_TRI;
+        pl.kernel = RBH_STREAM_TRI && RBH_STREAM64 && !p.materialise ? PLAN_STREAM_TRI : PLAN_WIDE_TRI;   // as launch_wide_tri
         pl.tiles = wide_tiles();
         pl.splitk = choose_split(pl.tiles, p.K / BK, p.split_req);
     } else if (stream_ok<T>(p)) {
