@@ -1176,6 +1176,9 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
 //    round, so the draw is spread evenly over the four SIMDs and the waves meet once per round.
 // Requires K % (128 / sizeof(T)) == 0, a memory operand with 16-B aligned rows contiguous along k
 // (mode 2), pc0 % 4 == 0, and the wave's 128 rows addressable with 32-bit byte offsets.
+#ifndef RBH_STREAM_ZMAJOR
+#define RBH_STREAM_ZMAJOR 0
+#endif
 #ifndef RBH_STREAM_PARTS64
 #define RBH_STREAM_PARTS64 2   // f64 64 x 512: a step in two 16-B parts (variant builds: 1)
 #endif
@@ -1223,7 +1226,11 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     const int64_t b = blockIdx.x;
     const int64_t xcd = b % 8, qq = nb / 8, rr = nb % 8;
     const int64_t t_all = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + b / 8;
+#if RBH_STREAM_ZMAJOR
+    const int64_t z = t_all / (nTg * nTm), t = t_all % (nTg * nTm);   // (variant: each split on its own XCDs)
+#else
     const int64_t z = t_all % split, t = t_all / split;
+#endif
     // consecutive tiles share a memory tile (the generated tiles of one memory tile run on one XCD)
     const int64_t go0 = (t % nTg) * BG, mo0 = (t / nTg) * (8 * BMW);
     const int64_t wm0 = mo0 + (int64_t)wave * BMW;        // this wave's first memory row

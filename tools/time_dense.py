@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--n", type=int, default=16384)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--splitk", type=int, default=0, help="rbh_options.splitk (0 = the library's choice)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     tdt = torch.float64 if a.dtype == "f64" else torch.float32
@@ -28,9 +29,10 @@ def main():
     rb.fill_dense("C", rb.DenseDist(a.m, a.n), a.m, a.n, 0, 0, A, rb.RNGState(99))
     S = rb.DenseSkOp(rb.DenseDist(a.d, a.m), rb.RNGState(0))
     B = torch.empty(a.d * a.n, dtype=tdt, device=dev)
+    opts = rb.Options(splitk=a.splitk)
 
     def call():
-        rb.sketch_general_left("C", "N", "N", a.d, a.n, a.m, 1.0, S, A, a.m, 0.0, B, a.d)
+        rb.sketch_general_left("C", "N", "N", a.d, a.n, a.m, 1.0, S, A, a.m, 0.0, B, a.d, options=opts)
 
     for _ in range(a.warmup):
         call()
@@ -42,7 +44,7 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.reps
-    plan = rb.plan_left("C", "N", "N", a.d, a.n, a.m, S, A, a.m, a.d, dtype=a.dtype)
+    plan = rb.plan_left("C", "N", "N", a.d, a.n, a.m, S, A, a.m, a.d, dtype=a.dtype, options=opts)
     flops = 2.0 * a.d * a.m * a.n
     peak = 78.6e12 if a.dtype == "f64" else 157.3e12
     print(json.dumps({"dtype": a.dtype, "d": a.d, "m": a.m, "n": a.n, "ms": ms, "tflops": flops / ms / 1e9,
