@@ -1182,6 +1182,18 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
 #ifndef RBH_STREAM_PARTS64
 #define RBH_STREAM_PARTS64 2   // f64 64 x 512: a step in two 16-B parts (variant builds: 1)
 #endif
+// Block-major part order (both 16-B halves of a lane's 32 B of a row's line loaded back to back). With
+// part-major order the second half was requested half a step after the first, and at a row stride of
+// 128 KiB (f32, m = 32768: every row of a step on the same L2 sets) the line was often gone by then:
+// C4 fetched 21.4-22.8 GB from beyond L2 per launch against |A| = 4.3 GB, 10.0-10.2 GB block-major,
+// kernel 4.50 -> 4.40 ms (same box, two alternations; profiles/r04/fetch_c4_order.txt). f64 (C2, whose
+// part-major order already fetches |A| once) measured 0.8 % slower block-major, so it keeps its order.
+#ifndef RBH_STREAM_CMAJOR32
+#define RBH_STREAM_CMAJOR32 1
+#endif
+#ifndef RBH_STREAM_CMAJOR64
+#define RBH_STREAM_CMAJOR64 0
+#endif
 template <typename T, int GK, int FAMILY, bool GX, bool SPLIT, int PF, int BG, int MW, int TRI = 0>
 __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     constexpr int KS = 128 / (int)sizeof(T);              // k per step
@@ -1202,6 +1214,15 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     constexpr int NH = NPART * FB;                        // part-blocks of a step (part FB + c)
     constexpr int NSLOT = PF + 1;                         // register slots of the memory prefetch ring
     static_assert(NH % NSLOT == 0, "a part-block's slot must not depend on the step");
+    // consumption order of a step's part-blocks: part-major (part p of every block, then part p + 1)
+    // or block-major (CMAJOR: both parts of block c, then block c + 1); every accumulator sees the same
+    // k order either way (its block's parts in turn), so the sums are the same bits
+    // (not for the f32 GEN_OO right-sketch form without split: it sits at 256 registers already and
+    // the second part's fragments would spill)
+    constexpr bool CMAJOR = NPART > 1 && (sizeof(T) == 8 ? RBH_STREAM_CMAJOR64 : RBH_STREAM_CMAJOR32) &&
+                            !(sizeof(T) == 4 && GK == GEN_OO && !GX && !SPLIT);
+    // part-block (p FB + c, mload's numbering) consumed s-th in block-major order
+    auto seq_block = [](int s) -> int { return (s % NPART) * FB + s / NPART; };
     static_assert(512 % CPS == 0 && R % SPU == 0, "every lane's calls of a round: same row, steps u SPU + ts0");
     typedef typename Mfma<T>::v4 acc_t;
     typedef float v4f __attribute__((ext_vector_type(4)));
@@ -1412,7 +1433,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     for (int u = 0; u < WCALLS; ++u) draw(u, kt0, 0, kt1);
     if (kt0 < kt1) {
 #pragma unroll
-        for (int i = 0; i < PF; ++i) mload(i % NSLOT, i, kt0);
+        for (int i = 0; i < PF; ++i) mload(i % NSLOT, CMAJOR ? seq_block(i) : i, kt0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
@@ -1424,6 +1445,30 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
         for (int ts = 0; ts < R; ++ts) {
             const int64_t kt = kr0 + ts;
             if (kt >= kt1) break;
+            if (CMAJOR) {
+                // block-major: both parts of block c back to back, so the two 16-B halves a lane
+                // takes of its row's 128-B line are requested PF part-blocks apart, not half a step
+                hv_t gf[NPART][FA];
+#pragma unroll
+                for (int h = 0; h < NPART; ++h)
+#pragma unroll
+                    for (int a = 0; a < FA; ++a) gf[h][a] = gread(half, ts, a, h);
+#pragma unroll
+                for (int c = 0; c < FB; ++c)
+#pragma unroll
+                    for (int h = 0; h < NPART; ++h) {
+                        const int s = c * NPART + h, sn = s + PF;
+                        const int64_t ktn = sn < NH ? kt : (kt + 1 < kt1 ? kt + 1 : kt);
+                        mload(sn % NSLOT, seq_block(sn % NH), ktn);
+                        const hv_t &m = mv[s % NSLOT];
+#pragma unroll
+                        for (int e = 0; e < PV; ++e)
+#pragma unroll
+                            for (int a = 0; a < FA; ++a)
+                                acc[a][c] = GX ? Mfma<T>::mma(m[e], gf[h][a][e], acc[a][c])
+                                               : Mfma<T>::mma(gf[h][a][e], m[e], acc[a][c]);
+                    }
+            } else {
 #pragma unroll
             for (int h = 0; h < NPART; ++h) {
                 hv_t gf[FA];
@@ -1442,6 +1487,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
                         for (int a = 0; a < FA; ++a)
                             acc[a][c] = GX ? Mfma<T>::mma(m[e], gf[a][e], acc[a][c]) : Mfma<T>::mma(gf[a][e], m[e], acc[a][c]);
                 }
+            }
             }
             // the next round's generated tiles: every wave's share, spread over the round (f64: its
             // one call after step 1; f32: one call after every step)
