@@ -1188,6 +1188,13 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
 // C4 fetched 21.4-22.8 GB from beyond L2 per launch against |A| = 4.3 GB, 10.0-10.2 GB block-major,
 // kernel 4.50 -> 4.40 ms (same box, two alternations; profiles/r04/fetch_c4_order.txt). f64 (C2, whose
 // part-major order already fetches |A| once) measured 0.8 % slower block-major, so it keeps its order.
+// A scheduling barrier after each prefetch load (f32): with the buffer resource in SGPRs (no
+// waterfall loop around each load any more) the scheduler sank every load to its MFMAs and waited
+// on it at once. C4 4.37 -> 4.03 ms (80.0 -> 86.7 % of the f32 peak, same box, two alternations),
+// L2-miss bytes 9.3-9.7 -> 4.7 GB per launch; d = 1024, m = n = 16384: 74.5 -> 80.5 %.
+#ifndef RBH_STREAM_SB64
+#define RBH_STREAM_SB64 0
+#endif
 #ifndef RBH_STREAM_CMAJOR32
 #define RBH_STREAM_CMAJOR32 1
 #endif
@@ -1261,8 +1268,14 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     // the operand clamped to its last row; their outputs are discarded)
     const T *mptr = (const T *)mop.ptr;
     const int64_t wbase = TRI ? 0 : (wm0 < mnO ? wm0 : mnO - 1);
-    const __amdgpu_buffer_rsrc_t mrsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(mptr + wbase * mop.so), (short)0, -1, 0x00020000);
+    // The wave's base address, pinned to SGPRs: left to itself the compiler computed wm0 in VGPRs for
+    // the f32 instantiations (f64 not) and wrapped every buffer load of the loop in a readfirstlane
+    // waterfall loop (4 v_readfirstlane, 2 v_cmp and 5 SALU per load, 16 loads a step).
+    const uint64_t mbase = (uint64_t)(uintptr_t)(mptr + wbase * mop.so);
+    uint32_t mb_lo = __builtin_amdgcn_readfirstlane((uint32_t)mbase), mb_hi = __builtin_amdgcn_readfirstlane((uint32_t)(mbase >> 32));
+    asm volatile("" : "+s"(mb_lo), "+s"(mb_hi));
+    const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(uintptr_t)(((uint64_t)mb_hi << 32) | mb_lo), (short)0, -1, 0x00020000);
     // One-triangle operand (TRI 1-4, as skge_wide_kernel): element (o, k) is stored at rowbase(o) + k
     // inside the triangle and is the stored (k, o) outside; the resource is based at the matrix and
     // the launcher checks that every byte offset of the stored triangle fits in 32 bits.
@@ -1460,6 +1473,9 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
                         const int s = c * NPART + h, sn = s + PF;
                         const int64_t ktn = sn < NH ? kt : (kt + 1 < kt1 ? kt + 1 : kt);
                         mload(sn % NSLOT, seq_block(sn % NH), ktn);
+                        // keep the load here, PF part-blocks ahead of its use (the scheduler otherwise
+                        // sinks it next to its MFMAs and waits on it at once)
+                        if (sizeof(T) == 4 || RBH_STREAM_SB64) __builtin_amdgcn_sched_barrier(0);
                         const hv_t &m = mv[s % NSLOT];
 #pragma unroll
                         for (int e = 0; e < PV; ++e)
@@ -1480,6 +1496,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
                     const int i = h * FB + c, in = i + PF;
                     const int64_t ktn = in < NH ? kt : (kt + 1 < kt1 ? kt + 1 : kt);
                     mload(in % NSLOT, in % NH, ktn);
+                    if (sizeof(T) == 4 || RBH_STREAM_SB64) __builtin_amdgcn_sched_barrier(0);   // (as above)
                     const hv_t &m = mv[i % NSLOT];
 #pragma unroll
                     for (int e = 0; e < PV; ++e)
