@@ -1186,20 +1186,22 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
 // part-major order the second half was requested half a step after the first, and at a row stride of
 // 128 KiB (f32, m = 32768: every row of a step on the same L2 sets) the line was often gone by then:
 // C4 fetched 21.4-22.8 GB from beyond L2 per launch against |A| = 4.3 GB, 10.0-10.2 GB block-major,
-// kernel 4.50 -> 4.40 ms (same box, two alternations; profiles/r04/fetch_c4_order.txt). f64 (C2, whose
-// part-major order already fetches |A| once) measured 0.8 % slower block-major, so it keeps its order.
-// A scheduling barrier after each prefetch load (f32): with the buffer resource in SGPRs (no
-// waterfall loop around each load any more) the scheduler sank every load to its MFMAs and waited
-// on it at once. C4 4.37 -> 4.03 ms (80.0 -> 86.7 % of the f32 peak, same box, two alternations),
-// L2-miss bytes 9.3-9.7 -> 4.7 GB per launch; d = 1024, m = n = 16384: 74.5 -> 80.5 %.
-#ifndef RBH_STREAM_SB64
-#define RBH_STREAM_SB64 0
-#endif
+// kernel 4.50 -> 4.40 ms (same box, two alternations; profiles/r04/fetch_c4_order.txt). With the
+// scheduling barriers below: f32 the same time in either order with half the L2-miss bytes
+// block-major; f64 0.4 % faster block-major (before the barriers it measured 0.8 % slower).
 #ifndef RBH_STREAM_CMAJOR32
 #define RBH_STREAM_CMAJOR32 1
 #endif
 #ifndef RBH_STREAM_CMAJOR64
-#define RBH_STREAM_CMAJOR64 0
+#define RBH_STREAM_CMAJOR64 1
+#endif
+// A scheduling barrier after each prefetch load: with the buffer resource in SGPRs (no waterfall
+// loop around each load any more) the scheduler sank every f32 load to its MFMAs and waited on it at
+// once. f32: C4 4.37 -> 4.03 ms (80.0 -> 86.7 % of the f32 peak, same box, two alternations), L2-miss
+// bytes 9.3-9.7 -> 4.7 GB per launch; d = 1024, m = n = 16384: 74.5 -> 80.5 %. f64 (block-major):
+// C2 8.005-8.011 -> 7.976 ms (profiles/r04/ab_sched_barrier.txt).
+#ifndef RBH_STREAM_SB64
+#define RBH_STREAM_SB64 1
 #endif
 template <typename T, int GK, int FAMILY, bool GX, bool SPLIT, int PF, int BG, int MW, int TRI = 0>
 __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
