@@ -1730,13 +1730,25 @@ static hipError_t materialise(const GemmProblem &p, void **buf, hipStream_t s) {
     return e;
 }
 
+#ifndef RBH_STREAM_F64_BG32
+#define RBH_STREAM_F64_BG32 1
+#endif
+struct StreamGeom {
+    int bg;      // generated rows per tile
+    int mw;      // memory rows per wave (the tile's memory rows: 8 mw)
+    int split;
+};
+template <typename T> static StreamGeom stream_geom(const GemmProblem &p);
+
 template <int GK, int FAMILY, bool GX, int TRI = 0>
 static hipError_t launch_wide(const GemmProblem &p, hipStream_t s) {
     typedef double T;
     const int64_t gnO = GX ? p.M : p.N, mnO = GX ? p.N : p.M;
     const int64_t nb = ((gnO + 63) / 64) * ((mnO + 511) / 512);
     if (nb <= 0) return hipSuccess;
-    const int split = choose_split(nb, p.K / BK, p.split_req);
+    // split-K: the streamed kernel's (stream_geom), so a materialised window or a one-triangle operand
+    // gives the bits of the drawn full-storage call
+    const int split = stream_geom<T>(p).split;
     GemmProblem q = p;
     q.splitk = split;
     q.partial = nullptr;
@@ -1800,11 +1812,7 @@ static bool wide_ok(const GemmProblem &p) {
 // its half as many tiles leave the chip emptier: the choice minimises (workgroup waves) x (work per
 // workgroup), BG = 64 work priced at 0.93 of BG = 32's per row (that measurement). C4 (d = 256,
 // 128 tiles of 64 x 1024) takes BG = 64 with split 2 (256 workgroups).
-struct StreamGeom {
-    int bg;      // generated rows per tile
-    int mw;      // memory rows per wave (the tile's memory rows: 8 mw)
-    int split;
-};
+
 constexpr double STREAM_BG64_COST = 0.93;
 template <typename T>
 static StreamGeom stream_geom(const GemmProblem &p) {
@@ -1813,7 +1821,17 @@ static StreamGeom stream_geom(const GemmProblem &p) {
     const int64_t nk = p.K / BK;   // 16-deep steps, as the 64 x 512 kernels count them
     const int64_t wide = ((gnO + 63) / 64) * ((mnO + 511) / 512);
     const int s32 = choose_split(wide, nk, p.split_req);
-    if (sizeof(T) == 8) return {64, 64, s32};   // the wide kernel's 64 x 512 tiles
+    if (sizeof(T) == 8) {   // the wide kernel's 64 x 512 tiles
+        // a small grid (split-K 8 or more over 64 x 512 tiles) takes 32 x 512 tiles, half the split:
+        // the same workgroups, half the partial sums written and re-read by the reduction (C1:
+        // 67 MB -> 34 MB per call)
+        if (RBH_STREAM_F64_BG32 && s32 >= 8 && p.split_req == 0) {
+            const int64_t t32 = ((gnO + 31) / 32) * ((mnO + 511) / 512);
+            const int sh = choose_split(t32, nk, 0);
+            if (sh < s32 && t32 * sh >= wide * s32) return {32, 64, sh};
+        }
+        return {64, 64, s32};
+    }
     if (RBH_STREAM_BG32 != 64) return {32, 128, s32};
     const int64_t t64 = ((gnO + 63) / 64) * ((mnO + 1023) / 1024), t32 = ((gnO + 31) / 32) * ((mnO + 1023) / 1024);
     const int s64 = choose_split(t64, nk, p.split_req);
@@ -1923,7 +1941,9 @@ static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
     const dim3 grid((unsigned)(nb * split));
     constexpr int PF = TRI ? RBH_STREAM_PF_TRI : stream_pf<T>();
     if constexpr (sizeof(T) == 8) {   // 64 x 512 tiles (64 x 1024 would take 256 accumulator registers)
-        if (split > 1) hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, PF, 64, 64, TRI>), grid, dim3(512), 0, s, q);
+        if (!TRI && gm.bg == 32) {   // small grids: 32 x 512 tiles (stream_geom), split K
+            hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, 3, 32, 64, 0>), grid, dim3(512), 0, s, q);
+        } else if (split > 1) hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, PF, 64, 64, TRI>), grid, dim3(512), 0, s, q);
         else hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, PF, 64, 64, TRI>), grid, dim3(512), 0, s, q);
     } else if (gm.bg == 64) {
         if (split > 1) hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, PF, 64, 128>), grid, dim3(512), 0, s, q);
@@ -2030,7 +2050,7 @@ static GemmPlan plan_gemm(const GemmProblem &p) {
     if (p.tri) {
         pl.kernel = RBH_STREAM_TRI && RBH_STREAM64 && !p.materialise ? PLAN_STREAM_TRI : PLAN_WIDE_TRI;   // as launch_wide_tri
         pl.tiles = wide_tiles();
-        pl.splitk = choose_split(pl.tiles, p.K / BK, p.split_req);
+        pl.splitk = stream_geom<T>(p).split;   // as launch_wide
     } else if (stream_ok<T>(p)) {
         const bool gx = p.xkind != MEM;
         const int64_t gnO = gx ? p.M : p.N, mnO = gx ? p.N : p.M;
@@ -2041,7 +2061,7 @@ static GemmPlan plan_gemm(const GemmProblem &p) {
     } else if (wide_ok<T>(p)) {
         pl.kernel = PLAN_WIDE;
         pl.tiles = wide_tiles();
-        pl.splitk = choose_split(pl.tiles, p.K / BK, p.split_req);
+        pl.splitk = stream_geom<T>(p).split;   // as launch_wide
     } else if (wide32_ok<T>(p)) {
         pl.kernel = PLAN_WIDE32;
         pl.tiles = wide_tiles();

@@ -313,7 +313,7 @@ def test_materialised_equals_drawn_bitwise(cuda, dtype):
 
 # Split-K on the wide kernels (What the multi-GPU dense runs execute: a rank's column chunk of
 # BASELINE configs[3] has 64 wide tiles and runs the f32 32-deep kernel split 4). d = 128, m = n =
-# 4096: 16 output tiles at K = 4096 -> automatic split 16; forced 1 (unsplit) and 3 (uneven
+# 4096: automatic split 16 (f32) / 8 (f64, 32 x 512 tiles); forced 1 (unsplit) and 3 (uneven
 # slices). RowMajor with opA = T keeps A contiguous along the contracted index (the wide kernels'
 # memory operand). Within E of the oracle; the plan names the kernel that ran.
 @pytest.mark.parametrize("dtype,kernel", [(np.float32, "stream"), (np.float64, "stream")])
@@ -328,7 +328,9 @@ def test_wide_split_k_within_bound(cuda, dtype, kernel, layout, opA, split):
                         dtype="f64" if dtype == np.float64 else "f32", options=opts)
     # (f64 builds without the streamed kernel run the 64 x 512 LDS kernel: the same tiles and sums)
     assert plan.kernel in ((kernel, "wide") if dtype == np.float64 else (kernel,)), plan
-    assert plan.splitk == (16 if split == 0 else split), plan
+    # automatic split: f32 16 over 16 tiles of 64 x 1024; f64 8 over 32 tiles of 32 x 512 (a small
+    # f64 grid takes the half-height tiles and half the split, stream_geom)
+    assert plan.splitk == ((8 if dtype == np.float64 else 16) if split == 0 else split), plan
     check_left(cuda, layout, "N", opA, d, n, m, 1.0, -0.5, d + 4, m, 4, 0, dtype, options=opts)
 
 
