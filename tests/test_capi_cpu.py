@@ -130,8 +130,8 @@ def test_plan_baseline_configs():
     assert _plan(1024, 16384, 16384, dtype="f32") == rb.Plan("stream", 1, 256, 256)
     # too little K to split: 256 tiles of 32 x 1024 beat 128 of 64 x 1024
     assert _plan(256, 32768, 1024, dtype="f32") == rb.Plan("stream", 1, 256, 256)
-    # C1: 16 tiles -> 16 slices of K = 4096
-    assert _plan(128, 4096, 4096) == rb.Plan("stream", 16, 16, 256)
+    # C1: 16 tiles of 64 x 512 would split 16 ways; 32 tiles of 32 x 512 split 8 (the same 256 workgroups)
+    assert _plan(128, 4096, 4096) == rb.Plan("stream", 8, 32, 256)
     # the north star split over 8 ranks: 128 tiles fill half the chip -> split 2
     assert _plan(256, 16384, 16384, D_rows=2048, ro=1792) == rb.Plan("stream", 2, 128, 256)
     # a quarter of C4's rank columns alone would split 8: the sharded driver passes the whole split

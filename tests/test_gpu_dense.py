@@ -359,9 +359,11 @@ def test_f32_split_chunks_bitwise_with_whole_split(cuda):
 # output element's terms in the same MFMA order as the 64 x 512 wide kernels, which the
 # materialised-window option still runs: bitwise equal across operand orientations (left/right x
 # layouts: the generated operand as X or Y), counter directions (major axis), families, ragged tiles,
-# split-K, and both streamed tile heights (f32 "bg64": 64 x 1024 tiles unsplit, "bg64split": split 16).
+# split-K, and both streamed tile heights (f32 "bg64": 64 x 1024 tiles unsplit, "bg64split": split 16;
+# f64 "f64bg32split": a small grid on 32 x 512 tiles, 24 tiles split 10 against the 64 x 512 wide
+# kernel's 12 tiles run with that split).
 STREAM_SHAPES = {"ragged": (100, 2100, 256), "split": (64, 1100, 4096), "bg64": (1000, 9000, 256),
-                 "bg64split": (250, 4000, 4096)}
+                 "bg64split": (250, 4000, 4096), "f64bg32split": (122, 3000, 4096)}
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
@@ -370,6 +372,8 @@ STREAM_SHAPES = {"ragged": (100, 2100, 256), "split": (64, 1100, 4096), "bg64": 
 @pytest.mark.parametrize("shape", sorted(STREAM_SHAPES))
 def test_stream_kernel_equals_wide_bitwise(cuda, dtype, side, layout, fam, maj, shape):
     d, n, m = STREAM_SHAPES[shape]
+    if shape.startswith("f64") and dtype != np.float64:
+        pytest.skip("an f64 tile-geometry case")
     tag = "f64" if dtype == np.float64 else "f32"
     ut = np.uint64 if dtype == np.float64 else np.uint32
     out, plans = [], []
@@ -399,9 +403,12 @@ def test_stream_kernel_equals_wide_bitwise(cuda, dtype, side, layout, fam, maj, 
         pytest.skip("f64 runs the 64 x 512 wide kernel (this build does not stream f64)")
     assert plans[0].kernel == "stream" and plans[1].kernel in ("wide", "wide32"), plans
     assert plans[0].splitk == plans[1].splitk and (plans[0].splitk > 1) == shape.endswith("split"), plans
-    if dtype == np.float32:   # (f64 streams 64 x 512 tiles)
+    if dtype == np.float32:
         bg = 64 if shape.startswith("bg64") else 32
         assert plans[0].tiles == -(-(d) // bg) * -(-n // 1024), plans
+    else:   # 64 x 512 tiles, or 32 x 512 where the 64 x 512 grid would split 8 or more ways
+        t64, t32 = -(-d // 64) * -(-n // 512), -(-d // 32) * -(-n // 512)
+        assert plans[0].tiles == (t32 if shape.startswith("f64bg32") else plans[0].tiles) and plans[0].tiles in (t64, t32), plans
     assert np.array_equal(out[0].view(ut), out[1].view(ut)), f"{np.sum(out[0] != out[1])} differ"
 
 
