@@ -1226,10 +1226,10 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     // consumption order of a step's part-blocks: part-major (part p of every block, then part p + 1)
     // or block-major (CMAJOR: both parts of block c, then block c + 1); every accumulator sees the same
     // k order either way (its block's parts in turn), so the sums are the same bits
-    // (not for the f32 GEN_OO right-sketch form without split: it sits at 256 registers already and
+    // (not for the f32 GEN_OO form with the generated operand as Y: it sits near 256 registers and
     // the second part's fragments would spill)
     constexpr bool CMAJOR = NPART > 1 && (sizeof(T) == 8 ? RBH_STREAM_CMAJOR64 : RBH_STREAM_CMAJOR32) &&
-                            !(sizeof(T) == 4 && GK == GEN_OO && !GX && !SPLIT);
+                            !(sizeof(T) == 4 && GK == GEN_OO && !GX) && !TRI;   // (one-triangle: as measured)
     // part-block (p FB + c, mload's numbering) consumed s-th in block-major order
     auto seq_block = [](int s) -> int { return (s % NPART) * FB + s / NPART; };
     static_assert(512 % CPS == 0 && R % SPU == 0, "every lane's calls of a round: same row, steps u SPU + ts0");
