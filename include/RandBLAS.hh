@@ -269,8 +269,8 @@ template <> struct Api<double> {
     }
     static constexpr auto lskge3 = rbh_lskge3_ex_f64;
     static constexpr auto rskge3 = rbh_rskge3_ex_f64;
-    static constexpr auto lskges = rbh_lskges_f64;
-    static constexpr auto rskges = rbh_rskges_f64;
+    static constexpr auto lskges = rbh_lskges_ex_f64;
+    static constexpr auto rskges = rbh_rskges_ex_f64;
     static constexpr auto sym = rbh_require_symmetric_f64;
     static constexpr auto lsksp3 = rbh_lsksp3_f64;
     static constexpr auto rsksp3 = rbh_rsksp3_f64;
@@ -285,8 +285,8 @@ template <> struct Api<float> {
     }
     static constexpr auto lskge3 = rbh_lskge3_ex_f32;
     static constexpr auto rskge3 = rbh_rskge3_ex_f32;
-    static constexpr auto lskges = rbh_lskges_f32;
-    static constexpr auto rskges = rbh_rskges_f32;
+    static constexpr auto lskges = rbh_lskges_ex_f32;
+    static constexpr auto rskges = rbh_rskges_ex_f32;
     static constexpr auto sym = rbh_require_symmetric_f32;
     static constexpr auto lsksp3 = rbh_lsksp3_f32;
     static constexpr auto rsksp3 = rbh_rsksp3_f32;
@@ -385,6 +385,10 @@ struct SparseSkOp {
     const RNGState<RNG> next_state;
     const bool own_memory = true;
     bool known_filled = false;
+    // Extension: the arrays hold this header's fill_sparse(S) output. For device arrays the apply
+    // then tells the library so (rbh_options.sparse_filled) and does not wait for its device check;
+    // clear it after writing to the arrays yourself (a false claim makes the sketch NaN).
+    bool filled_by_library = false;
     sint_t *rows = nullptr;
     sint_t *cols = nullptr;
     T *vals = nullptr;
@@ -432,6 +436,7 @@ void fill_sparse(SparseSkOpT &S) {
     const rbh_state s = detail::c_state(S.seed_state);
     detail::check(detail::Api<T>::fill_sparse(&d, &s, S.rows, S.cols, S.vals));
     S.known_filled = true;
+    S.filled_by_library = true;
 }
 
 namespace sparse_data {
@@ -492,6 +497,16 @@ void lsk(blas::Layout layout, blas::Op opS, blas::Op opA, int64_t d, int64_t n, 
 // arrays hold exactly the device sampler's output, so the apply samples on the device again
 // (no host-to-device copy of the COO arrays); an operator that arrived filled is applied from
 // its arrays. Afterwards the arrays are permuted as the reference's COO apply leaves them.
+// Device arrays this header filled are passed with rbh_options.sparse_filled (no host wait for
+// the fast apply's check); host arrays are staged by a synchronous call anyway, so they keep the
+// checked form (a modified host array then falls back instead of failing).
+template <typename T, typename RNG, typename sint_t>
+rbh_options sparse_options(const SparseSkOp<T, RNG, sint_t> &S, T alpha) {
+    rbh_options o = ext::thread_options();
+    if (S.filled_by_library && (alpha == (T)1 || alpha == (T)-1) && S.vals && rbh_is_device_pointer(S.vals))
+        o.sparse_filled = 1;
+    return o;
+}
 template <typename T, typename RNG, typename sint_t>
 void lsk(blas::Layout layout, blas::Op opS, blas::Op opA, int64_t d, int64_t n, int64_t m, T alpha,
          SparseSkOp<T, RNG, sint_t> &S, int64_t ro_s, int64_t co_s, const T *A, int64_t lda, T beta, T *B,
@@ -500,9 +515,10 @@ void lsk(blas::Layout layout, blas::Op opS, blas::Op opA, int64_t d, int64_t n, 
     const rbh_state s = c_state(S.seed_state);
     const bool given = S.known_filled;
     if (!given) fill_sparse(S);
+    const rbh_options o = sparse_options(S, alpha);
     check(Api<T>::lskges((char)layout, (char)opS, (char)opA, d, n, m, alpha, &dd, &s, given ? S.nnz_count() : 0,
                          given ? S.rows : nullptr, given ? S.cols : nullptr, given ? S.vals : nullptr, ro_s, co_s, A,
-                         lda, beta, B, ldb, nullptr));
+                         lda, beta, B, ldb, &o, nullptr));
     // left_spmm views S transposed when opS == Trans (spmm_dispatch.hh:69-87)
     coo_sort_as_reference(S.nnz_count(), S.rows, S.cols, S.vals, opS == blas::Op::Trans);
 }
@@ -521,9 +537,10 @@ void rsk(blas::Layout layout, blas::Op opA, blas::Op opS, int64_t m, int64_t d, 
     const rbh_state s = c_state(S.seed_state);
     const bool given = S.known_filled;
     if (!given) fill_sparse(S);
+    const rbh_options o = sparse_options(S, alpha);
     check(Api<T>::rskges((char)layout, (char)opA, (char)opS, m, d, n, alpha, A, lda, &dd, &s,
                          given ? S.nnz_count() : 0, given ? S.rows : nullptr, given ? S.cols : nullptr,
-                         given ? S.vals : nullptr, ro_s, co_s, beta, B, ldb, nullptr));
+                         given ? S.vals : nullptr, ro_s, co_s, beta, B, ldb, &o, nullptr));
     // right_spmm calls left_spmm with opS flipped (spmm_dispatch.hh:194-199): transposed view iff NoTrans
     coo_sort_as_reference(S.nnz_count(), S.rows, S.cols, S.vals, opS == blas::Op::NoTrans);
 }

@@ -66,13 +66,15 @@ void rbh_kernel_timing_enable(int on);
 int rbh_kernel_timing_collect(float *ms, int max);
 
 /* Workspaces (no reference counterpart): the library keeps the device blocks its calls carve
- * workspaces from, one arena per (device, stream), so repeated calls pay no allocation. This
- * synchronises `stream` and frees its arena's idle blocks (stream NULL: the null stream's arena);
- * all_streams != 0 synchronises the device and does so for every stream of the current device (call
- * it after destroying streams the library has seen). The library also releases idle blocks by
- * itself before its retained bytes on a device would pass 2 GiB (not while the calling stream is
- * being captured into a graph). */
-int rbh_release_workspaces(void *stream, int all_streams);
+ * workspaces from, one arena per (device, stream), so repeated calls pay no allocation.
+ * rbh_release_workspaces_ex synchronises `stream` and frees its arena's idle blocks (stream NULL:
+ * the null stream's arena); all_streams != 0 synchronises the device and does so for every stream
+ * of the current device (call it after destroying streams the library has seen).
+ * rbh_release_workspaces is the ABI-1 form, unchanged: NULL = every stream of the device, a stream
+ * = that stream's arena. The library also releases idle blocks by itself before its retained bytes
+ * on a device would pass 2 GiB (not while the calling stream is being captured into a graph). */
+int rbh_release_workspaces(void *stream);
+int rbh_release_workspaces_ex(void *stream, int all_streams);
 
 /* Shard reassembly for multi-GPU sketching (no reference counterpart): an
  * all-gather leaves nshards shards one after another, shard g being `rows` runs of `run` elements;
@@ -152,9 +154,12 @@ int rbh_rskge3_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_
  *                  arrays are fill_sparse's output for this operator, unmodified. Arrays whose
  *                  in-window values alpha * v are all +-1 with no repeated (row, k) -- every
  *                  fill_sparse output applied with |alpha| = 1 -- take the fast LDS-DMA apply after
- *                  a device check: with 0 (default) the call waits for that check (and falls back to
- *                  the sorted apply when it fails); with 1 it does not wait, and a failed check
- *                  makes the sketch NaN. */
+ *                  a device check: with 0 (default) the call waits for that check on the host (and
+ *                  falls back to the sorted apply when it fails; on a stream being captured into a
+ *                  graph, where it cannot wait, it takes the sorted apply directly); with 1 it does
+ *                  not wait, and a failed check makes the sketch NaN. The claim is honoured only
+ *                  with |alpha| = 1 (fill_sparse's values are +-1); with any other alpha the call
+ *                  waits as with 0. */
 typedef struct rbh_options {
     int32_t splitk;
     int32_t materialise;

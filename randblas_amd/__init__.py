@@ -126,7 +126,8 @@ for _t, _ct in (("f64", ctypes.c_double), ("f32", ctypes.c_float)):
                                                       P(DenseDistC), c_vp, c_char, c_i64, c_i64, c_i64, P(OptionsC),
                                                       P(PlanC)]
 lib.rbh_is_device_pointer.argtypes = [c_vp]
-lib.rbh_release_workspaces.argtypes = [c_vp, ctypes.c_int]
+lib.rbh_release_workspaces.argtypes = [c_vp]
+lib.rbh_release_workspaces_ex.argtypes = [c_vp, ctypes.c_int]
 lib.rbh_sketch_symmetric_last_path.restype = ctypes.c_int
 lib.rbh_sparse_last_path.restype = ctypes.c_int
 SPARSE_PATHS = {0: "none", 1: "dma", 2: "gather", 3: "sorted_unit", 4: "sorted"}
@@ -257,6 +258,7 @@ class SparseSkOp:
     vals: object = None
     nnz: Optional[int] = None
     filled_by_library: bool = False   # the arrays are fill_sparse(S)'s own output (set by fill_sparse_op)
+    _fill_versions: tuple = field(default=(), repr=False)   # _array_versions(S) right after that fill
 
     @property
     def n_rows(self):
@@ -368,9 +370,18 @@ def fill_sparse(S: SparseSkOp, rows, cols, vals, stream=None) -> None:
               _stream(vals, stream)))
 
 
-def _sparse_opts(S, options):
-    """A SparseSkOp whose arrays fill_sparse_op wrote: tell the library (sparse_filled)."""
-    if S.rows is not None and S.filled_by_library:
+def _array_versions(S):
+    """(identity, in-place version) of S's three arrays: torch counts every in-place write of a
+    tensor in `_version`, so a changed tuple means the arrays are no longer fill_sparse's output."""
+    return tuple((id(a), getattr(a, "_version", None)) for a in (S.rows, S.cols, S.vals))
+
+
+def _sparse_opts(S, options, alpha):
+    """A SparseSkOp whose arrays fill_sparse_op wrote and nobody has written since: tell the
+    library (sparse_filled), which then does not wait for its device check. Only with |alpha| = 1:
+    the claim means "every alpha * v is +-1", and fill_sparse's values are +-1."""
+    if (S.rows is not None and S.filled_by_library and alpha in (1.0, -1.0)
+            and S._fill_versions == _array_versions(S)):
         o = options or Options()
         return Options(o.splitk, o.materialise, o.sksy_triangle, True)
     return options
@@ -392,6 +403,7 @@ def fill_sparse_op(S: SparseSkOp, dtype="f64", device=None, stream=None) -> Spar
     S.nnz = nnz
     fill_sparse(S, S.rows, S.cols, S.vals, stream)
     S.filled_by_library = True
+    S._fill_versions = _array_versions(S)
     return S
 
 
@@ -411,7 +423,7 @@ def sketch_general_left(layout, opS, opA, d, n, m, alpha, S, A, lda, beta, B, ld
         nnz = S.nnz if S.nnz is not None else (S.dist.nnz if S.rows is not None else 0)
         _check(fn(_b(layout), _b(opS), _b(opA), d, n, m, alpha, ctypes.byref(S.dist.c()),
                   ctypes.byref(S.seed_state.c()), nnz, _ptr(S.rows), _ptr(S.cols), _ptr(S.vals), ro_s, co_s, _ptr(A),
-                  lda, beta, _ptr(B), ldb, _opt(_sparse_opts(S, options)), st))
+                  lda, beta, _ptr(B), ldb, _opt(_sparse_opts(S, options, alpha)), st))
     else:
         raise TypeError("S must be a DenseSkOp or SparseSkOp")
 
@@ -431,7 +443,7 @@ def sketch_general_right(layout, opA, opS, m, d, n, alpha, A, lda, S, beta, B, l
         nnz = S.nnz if S.nnz is not None else (S.dist.nnz if S.rows is not None else 0)
         _check(fn(_b(layout), _b(opA), _b(opS), m, d, n, alpha, _ptr(A), lda, ctypes.byref(S.dist.c()),
                   ctypes.byref(S.seed_state.c()), nnz, _ptr(S.rows), _ptr(S.cols), _ptr(S.vals), ro_s, co_s, beta,
-                  _ptr(B), ldb, _opt(_sparse_opts(S, options)), st))
+                  _ptr(B), ldb, _opt(_sparse_opts(S, options, alpha)), st))
     else:
         raise TypeError("S must be a DenseSkOp or SparseSkOp")
 
@@ -665,7 +677,7 @@ def release_workspaces(stream=None, all_streams: Optional[bool] = None) -> None:
         stream = stream.cuda_stream
     if all_streams is None:
         all_streams = stream is None
-    _check(lib.rbh_release_workspaces(c_vp(stream) if stream else None, 1 if all_streams else 0))
+    _check(lib.rbh_release_workspaces_ex(c_vp(stream) if stream else None, 1 if all_streams else 0))
 
 
 def unpack_shards(src, nshards, rows, run, dst, row_stride, shard_stride, stream=None) -> None:

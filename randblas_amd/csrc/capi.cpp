@@ -1250,9 +1250,8 @@ int sketch_symmetric(char layout, char side, int64_t d, int64_t n, T alpha, cons
     RBH_HIP(st.map_out(B, sizeof(T), layout, side == 'L' ? d : n, side == 'L' ? n : d, ldb, beta != (T)0, &dB));
     RBH_HIP(st.map(S_buff, sizeof(T) * D->n_rows * D->n_cols, true, false, &dS));
     const bool use_tri = opt && opt->sksy_triangle;
-    g_sksy_path = 0;
-    if (!(flags & 2) && use_tri) {
-        g_sksy_path = 1;
+    const int path = (!(flags & 2) && use_tri) ? 1 : 0;
+    if (path == 1) {
         rc = sksy_tri_dev<T>(layout, side, 'U', 'F', d, n, alpha, D, seed, dS, S_layout, ro_s, co_s, dA, lda, beta,
                              dB, ldb, opt, s);
     } else {
@@ -1266,6 +1265,7 @@ int sketch_symmetric(char layout, char side, int64_t d, int64_t n, T alpha, cons
     }
     if (rc) return rc;
     RBH_HIP(st.finish());
+    g_sksy_path = path;   // the last *successful* call's storage path
     return RBH_OK;
 }
 
@@ -1305,13 +1305,16 @@ int dense_plan(bool left, char layout, char opS, char opA, int64_t M1, int64_t M
 // =============================================================================================
 extern "C" {
 
-int rbh_abi_version(void) { return 2; }
+int rbh_abi_version(void) { return 3; }
 
-int rbh_release_workspaces(void *stream, int all_streams) {
+int rbh_release_workspaces_ex(void *stream, int all_streams) {
     const hipError_t e = ws_release((hipStream_t)stream, all_streams != 0);
     if (e != hipSuccess) return set_error(RBH_ERR_HIP, "HIP error %s in rbh_release_workspaces", hipGetErrorName(e));
     return RBH_OK;
 }
+
+// the ABI-1 form: NULL = every stream of the device, otherwise that stream's arena
+int rbh_release_workspaces(void *stream) { return rbh_release_workspaces_ex(stream, stream == nullptr); }
 
 int rbh_unpack_shards(const void *src, int64_t nshards, int64_t rows, int64_t run, void *dst, int64_t row_stride,
                       int64_t shard_stride, int elem_bytes, void *stream) {

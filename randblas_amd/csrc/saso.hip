@@ -1708,9 +1708,22 @@ static hipError_t run_sparse_apply_t(const SparseApply &p, const int64_t *rows, 
         // with |alpha| = 1, the reference's fill-once / apply-many use (skge.hh:503-504,
         // sparse_skops.hh:389-413) -- which mark_check_kernel verifies on the device
         bool y_k;
-        const bool values_can_be_unit = !p.unit_vals || p.alpha == 1.0 || p.alpha == -1.0;
-        if (sizeof(T) == 8 && nnz > 0 && values_can_be_unit && dma_layout_ok(p, y_k)) {
-            const hipError_t e = run_sparse_dma(p, nullptr, rows, cols, (const double *)vals, nnz, y_k, s);
+        const bool unit_alpha = p.alpha == 1.0 || p.alpha == -1.0;
+        const bool values_can_be_unit = !p.unit_vals || unit_alpha;
+        SparseApply q = p;
+        // The filled claim says "fill_sparse's unmodified output", i.e. values +-1: it vouches for
+        // alpha * v = +-1 only when |alpha| = 1. Otherwise the check's result is waited for.
+        if (!unit_alpha) q.arrays_filled = 0;
+        // Waiting for the check is a host synchronisation, which a capturing stream cannot do:
+        // unclaimed arrays then take the sorted path, which needs no wait.
+        bool capturing = false;
+        if (!q.arrays_filled) {
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            if (hipStreamIsCapturing(s, &cs) != hipSuccess) { (void)hipGetLastError(); cs = hipStreamCaptureStatusNone; }
+            capturing = cs != hipStreamCaptureStatusNone;
+        }
+        if (sizeof(T) == 8 && nnz > 0 && values_can_be_unit && !capturing && dma_layout_ok(q, y_k)) {
+            const hipError_t e = run_sparse_dma(q, nullptr, rows, cols, (const double *)vals, nnz, y_k, s);
             if (e != hipErrorNotSupported) return e;   // NotSupported: check failed / too many records
         }
     }

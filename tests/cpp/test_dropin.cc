@@ -6,6 +6,7 @@
 // host buffers, and compare with an explicit product of the materialised operator.
 // Built and run by tests/test_gpu_cpp_dropin.py; prints "ALL PASSED" on success.
 #include <RandBLAS.hh>
+#include <hip/hip_runtime_api.h>
 
 #include <algorithm>
 #include <cmath>
@@ -519,6 +520,62 @@ static void namespaced_entry_points() {
     }
 }
 
+// A filled SparseSkOp applied twice from its arrays takes the LDS-DMA apply (rbh_sparse_last_path
+// 1) with the bits of the first apply: host arrays (checked on the device, the synchronous call
+// waits for the check) and hipMalloc arrays this header filled (rbh_options.sparse_filled: no
+// wait). With alpha = 2 the filled claim does not hold and the call takes the checked fallback;
+// arrays the caller rewrote (filled_by_library cleared) are checked again.
+static void filled_operator_fast_path() {
+    const int64_t d = 64, m = 1500, n = 40;
+    RandBLAS::SparseDist D{d, m, 4};
+    auto A = random_matrix<double>(m, n, 99);
+    std::vector<double> B1(d * n), B2(d * n);
+    RandBLAS::SparseSkOp<double> S(D, 5);
+    RandBLAS::fill_sparse(S);
+    CHECK(S.known_filled && S.filled_by_library);
+    RandBLAS::sketch_general(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, m, 1.0, S, A.data(), m, 0.0, B1.data(), d);
+    CHECK(rbh_sparse_last_path() == 1);
+    RandBLAS::sketch_general(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, m, 1.0, S, A.data(), m, 0.0, B2.data(), d);
+    CHECK(rbh_sparse_last_path() == 1);
+    for (int64_t e = 0; e < d * n; ++e) CHECK(B2[e] == B1[e]);
+
+    const int64_t nnz = S.nnz_count();
+    int64_t *dr = nullptr, *dc = nullptr;
+    double *dv = nullptr, *dA = nullptr, *dB = nullptr;
+    CHECK(hipMalloc((void **)&dr, nnz * sizeof(int64_t)) == hipSuccess);
+    CHECK(hipMalloc((void **)&dc, nnz * sizeof(int64_t)) == hipSuccess);
+    CHECK(hipMalloc((void **)&dv, nnz * sizeof(double)) == hipSuccess);
+    CHECK(hipMalloc((void **)&dA, m * n * sizeof(double)) == hipSuccess);
+    CHECK(hipMalloc((void **)&dB, d * n * sizeof(double)) == hipSuccess);
+    CHECK(hipMemcpy(dA, A.data(), m * n * sizeof(double), hipMemcpyHostToDevice) == hipSuccess);
+    RandBLAS::SparseSkOp<double> Sd(D, RandBLAS::RNGState<>(5), dr, dc, dv, false);
+    RandBLAS::fill_sparse(Sd);
+    CHECK(Sd.filled_by_library);
+    std::vector<double> Bd(d * n);
+    for (int rep = 0; rep < 2; ++rep) {
+        RandBLAS::sketch_general(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, m, 1.0, Sd, dA, m, 0.0, dB, d);
+        CHECK(rbh_sparse_last_path() == 1);
+        CHECK(hipMemcpy(Bd.data(), dB, d * n * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess);
+        for (int64_t e = 0; e < d * n; ++e) CHECK(Bd[e] == B1[e]);
+    }
+    // alpha = 2: every alpha * v is +-2, so the claim is not made and the checked fallback runs
+    RandBLAS::sketch_general(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, m, 2.0, Sd, dA, m, 0.0, dB, d);
+    CHECK(rbh_sparse_last_path() != 1);
+    CHECK(hipMemcpy(Bd.data(), dB, d * n * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess);
+    for (int64_t e = 0; e < d * n; ++e) CHECK(Bd[e] == 2.0 * B1[e]);
+    // values rewritten by the caller (+-1/2): the claim is withdrawn, and alpha = 2 makes them unit
+    std::vector<double> hv(nnz);
+    CHECK(hipMemcpy(hv.data(), dv, nnz * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess);
+    for (auto &v : hv) v *= 0.5;
+    CHECK(hipMemcpy(dv, hv.data(), nnz * sizeof(double), hipMemcpyHostToDevice) == hipSuccess);
+    Sd.filled_by_library = false;
+    RandBLAS::sketch_general(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, m, 2.0, Sd, dA, m, 0.0, dB, d);
+    CHECK(rbh_sparse_last_path() == 1);
+    CHECK(hipMemcpy(Bd.data(), dB, d * n * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess);
+    for (int64_t e = 0; e < d * n; ++e) CHECK(Bd[e] == B1[e]);
+    (void)hipFree(dr); (void)hipFree(dc); (void)hipFree(dv); (void)hipFree(dA); (void)hipFree(dB);
+}
+
 int main() {
 #ifdef ONLY_SKSP   // diagnostics: the sketch_sparse checks alone
     try {
@@ -543,6 +600,7 @@ int main() {
     spmm_both_sides();
     symmetric_one_triangle();
     namespaced_entry_points();
+    filled_operator_fast_path();
     if (g_fail) {
         std::printf("%d checks FAILED\n", g_fail);
         return 1;

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert rb.abi_version() == 2
+    assert rb.abi_version() == 3
 
 
 @pytest.mark.parametrize("dims", [(10, 37), (37, 10), (64, 64), (5, 3), (1024, 16384)])

@@ -308,3 +308,87 @@ def test_sparse_filled_claim_that_fails_the_check_gives_nan(cuda):
                            options=rb.Options(sparse_filled=True))
     assert rb.sparse_last_path() == "dma"
     assert bool(torch.isnan(dB).all())
+
+
+@pytest.mark.parametrize("alpha", [2.0, 0.5, -3.0])
+def test_filled_operator_with_non_unit_alpha(cuda, alpha):
+    """fill_sparse_op(S) applied with |alpha| != 1: every alpha * v is +-alpha, so the filled claim is
+    not made (Python) nor honoured (C); the checked fallback gives the oracle's bits, never NaN
+    (this returned NaN when the claim was passed whatever alpha was)."""
+    d, m, n = 256, 2048, 70
+    A = O.random_matrix(m, n, 99)
+    B0 = O.random_matrix(d, n, 42)
+    rows, cols, vals = O.fill_sparse(d, m, 8, "S", key=6)
+    Bexp = _oracle_left(d, n, m, alpha, rows, cols, vals, A, 0.5, B0)
+    S = rb.fill_sparse_op(rb.SparseSkOp(rb.SparseDist(d, m, 8), rb.RNGState(6)))
+    dB = dev(B0, cuda)
+    rb.sketch_general_left("C", "N", "N", d, n, m, alpha, S, dev(A, cuda), m, 0.5, dB, d)
+    assert rb.sparse_last_path() != "dma"
+    assert np.array_equal(bits(host(dB)), bits(Bexp))
+    # the C side alone: an explicit claim with alpha != +-1 is not honoured either
+    dB = dev(B0, cuda)
+    rb.sketch_general_left("C", "N", "N", d, n, m, alpha, S, dev(A, cuda), m, 0.5, dB, d,
+                           options=rb.Options(sparse_filled=True))
+    assert np.array_equal(bits(host(dB)), bits(Bexp))
+
+
+def test_filled_operator_modified_after_fill(cuda):
+    """S.vals written in place after fill_sparse_op (torch counts the write): the claim is withdrawn,
+    the device check runs and the result is the oracle's for the new values."""
+    d, m, n = 200, 1500, 40
+    A = O.random_matrix(m, n, 99)
+    rows, cols, vals = O.fill_sparse(d, m, 4, "S", key=8)
+    S = rb.fill_sparse_op(rb.SparseSkOp(rb.SparseDist(d, m, 4), rb.RNGState(8)))
+    S.vals[5] = 0.25   # in place: S.vals._version changes
+    vals = vals.copy()
+    vals[5] = 0.25
+    Bexp = _oracle_left(d, n, m, 1.0, rows, cols, vals, A, 0.0, np.zeros(d * n))
+    dB = torch.zeros(d * n, dtype=torch.float64, device=cuda)
+    rb.sketch_general_left("C", "N", "N", d, n, m, 1.0, S, dev(A, cuda), m, 0.0, dB, d)
+    assert rb.sparse_last_path() in ("sorted_unit", "sorted")
+    assert np.array_equal(bits(host(dB)), bits(Bexp))
+    S.vals.mul_(2.0)   # now +-2 (and 0.5): with alpha = 0.5 entry 5 is 0.25 -> still not unit
+    vals = vals * 2.0
+    Bexp = _oracle_left(d, n, m, 0.5, rows, cols, vals, A, 0.0, np.zeros(d * n))
+    rb.sketch_general_left("C", "N", "N", d, n, m, 0.5, S, dev(A, cuda), m, 0.0, dB, d)
+    assert np.array_equal(bits(host(dB)), bits(Bexp))
+
+
+def test_sketch_symmetric_with_filled_sparse_operator(cuda):
+    """sketch_symmetric with a filled SparseSkOp and alpha = 3 (routes through the sparse
+    sketch_general with the caller's alpha): the oracle's bits, not NaN."""
+    d, n = 64, 512
+    M = O.random_matrix(n, n, 7).reshape(n, n)
+    A = np.ascontiguousarray(0.5 * (M + M.T)).reshape(-1)
+    rows, cols, vals = O.fill_sparse(d, n, 4, "S", key=2)
+    Bexp = _oracle_left(d, n, n, 3.0, rows, cols, vals, A, 0.0, np.zeros(d * n))
+    S = rb.fill_sparse_op(rb.SparseSkOp(rb.SparseDist(d, n, 4), rb.RNGState(2)))
+    dB = torch.zeros(d * n, dtype=torch.float64, device=cuda)
+    rb.sketch_symmetric_left("C", d, n, 3.0, S, dev(A, cuda), n, 0.0, dB, d)
+    assert np.array_equal(bits(host(dB)), bits(Bexp))
+
+
+def test_unclaimed_arrays_under_graph_capture(cuda):
+    """Caller arrays of unknown origin on a stream being captured into a graph: the call cannot wait
+    for the device check there, so it takes the sorted apply (no host synchronisation); replaying
+    the graph gives the oracle's bits."""
+    d, m, n = 128, 1024, 64
+    A = O.random_matrix(m, n, 99)
+    rows, cols, vals = O.fill_sparse(d, m, 4, "S", key=12)
+    Bexp = _oracle_left(d, n, m, 1.0, rows, cols, vals, A, 0.0, np.zeros(d * n))
+    S = rb.SparseSkOp(rb.SparseDist(d, m, 4), rb.RNGState(12), dev(rows, cuda), dev(cols, cuda), dev(vals, cuda))
+    dA = dev(A, cuda)
+    dB = torch.zeros(d * n, dtype=torch.float64, device=cuda)
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):   # warm the stream's workspace arena (both paths) outside the capture
+        rb.sketch_general_left("C", "N", "N", d, n, m, 1.0, S, dA, m, 0.0, dB, d)
+        rb.sketch_general_left("C", "N", "N", d, n, m, 2.0, S, dA, m, 0.0, dB, d)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        rb.sketch_general_left("C", "N", "N", d, n, m, 1.0, S, dA, m, 0.0, dB, d)
+    assert rb.sparse_last_path() in ("sorted_unit", "sorted")
+    dB.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(host(dB)), bits(Bexp))
