@@ -24,11 +24,18 @@ Prints ONE JSON line (rank 0). value = d_total*n / t_step (entries/s, whole job)
 GEMM kernel's algorithmic flops (2*d*m*n per launch) / its average launch time measured with HIP
 events on the launch stream; cpu_baseline = the oracle's OpenMP fill + host BLAS dgemm (the
 reference's algorithm, oracle/) on a bounded column sample, rank 0 only.
+
+Without --config the line also carries "configs": every other BASELINE workload (NS, C3 sampled and
+pre-filled, C4 per GPU, C5, C5p, C1), each timed in this same process with the same steps and
+warm-up, after the headline, with its own ms_per_step, kernel_ms, roofline (traffic + its source),
+plan and a shorter CPU baseline. `--config X` times X alone as the line's top level. Sharded runs
+also report single_call_ms: one step timed alone, its whole all-gather included.
 """
 from __future__ import annotations
 
 import argparse
 import faulthandler
+import gc
 import json
 import os
 import sys
@@ -183,36 +190,254 @@ def relaunch(ngpus: int) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
-def shard_rows(args, world):
+def shard_rows(args, world, config):
     """(d_total, d_per_gpu, scaling) of a dense config: weak scaling keeps d rows per GPU (the job
     is the (world d) x n sketch); --split-d keeps the problem (D_TOTAL rows) and gives each rank
     D_TOTAL / world of them."""
-    kind, _, d, _, _, _ = CONFIGS[args.config]
+    kind, _, d, _, _, _ = CONFIGS[config]
     if not args.split_d:
         return (d if kind == "saso" else world * d), d, "weak"
     if kind == "saso":
         raise SystemExit("bench: --split-d applies to the dense configs (SASO shards by columns)")
-    total = D_TOTAL[args.config]
+    total = D_TOTAL[config]
     if total % world:
         raise SystemExit(f"bench: --split-d needs d = {total} divisible by the {world} ranks")
     return total, total // world, "strong"
 
 
-def dry_run(args, world, rank):
+def dry_run(args, world, rank, config, subs):
     """--dry-run: the launch / rendezvous / reporting path without device work (CPU, gloo):
     every rank joins, the max-over-ranks reduction runs, rank 0 prints the line's skeleton."""
-    d_total, d_loc, scaling = shard_rows(args, world)
+    d_total, d_loc, scaling = shard_rows(args, world, config)
     if world > 1:
         dist.init_process_group("gloo")
     t = torch.tensor([float(rank)], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     if rank == 0:
-        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_max": float(t.item()), "config": args.config,
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_max": float(t.item()), "config": config,
                           "steps": args.steps, "warmup": args.warmup, "d": d_total, "d_per_gpu": d_loc,
-                          "ro_s": [g * d_loc for g in range(world)], "scaling": scaling}), flush=True)
+                          "ro_s": [g * d_loc for g in range(world)], "scaling": scaling,
+                          "configs": [name for name, _, _ in subs]}), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+WORKLOADS = {"c1": "Gaussian skge fp64 d=128 A 4096^2 (BASELINE configs[0], the reference's CPU case)",
+             "c2": "Gaussian skge fp64 (BASELINE configs[1])",
+             "ns": "Gaussian skge fp64 north-star",
+             "c3": "SASO SparseSkOp vec_nnz=8 fp64 (configs[2])",
+             "c4": "Gaussian skge fp32 (configs[3])",
+             "c5": "sksy fp64, sketch_symmetric with sym_check_tol=0 (configs[4])",
+             "c5p": "sksy fp64 on packed-symmetric A (configs[4] as worded)"}
+
+# The configs a default run times after the headline (c2), each in this process with the same steps
+# and warm-up: (record name, config, SASO operator filled once before timing)
+SUB_CONFIGS = [("ns", "ns", False), ("c3", "c3", False), ("c3_prefilled", "c3", True), ("c4", "c4", False),
+               ("c5", "c5", False), ("c5p", "c5p", False), ("c1", "c1", False)]
+
+
+def run_config(args, config, prefilled, world, rank, dev, use_dist, cpu_target_s):
+    """Time args.steps steps of one workload (after args.warmup untimed ones) and return its record:
+    step time (max over ranks), the dominant kernel's event time and roofline, the plan, and (rank 0,
+    one GPU) the CPU baseline. The device memory of the workload is released before returning."""
+    gc.collect()               # the previous workload's tensors (freed when its call returned)
+    torch.cuda.empty_cache()
+    kind, dtype, d, m, n, vec_nnz = CONFIGS[config]
+    d_total, d, scaling = shard_rows(args, world, config)   # d: this rank's rows (dense) / all rows (SASO)
+    tdt = torch.float64 if dtype == "f64" else torch.float32
+
+    # A ~ DenseDist(m, n) Gaussian key 99, ColMajor, generated on the device (input, not timed).
+    # SASO shards by columns: rank g holds columns [g n, (g+1) n) of DenseDist(m, world n).
+    A = torch.empty(m * n, dtype=tdt, device=dev)
+    if kind == "saso":
+        rb.fill_dense("C", rb.DenseDist(m, world * n), m, n, 0, rank * n, A, rb.RNGState(99))
+        S = rb.SparseSkOp(rb.SparseDist(d, m, vec_nnz), rb.RNGState(0))
+        if prefilled:   # fill once (untimed), apply from the arrays every step (skge.hh:503-504)
+            rb.fill_sparse_op(S)
+    else:
+        rb.fill_dense("C", rb.DenseDist(m, n), m, n, 0, 0, A, rb.RNGState(99))
+        S = rb.DenseSkOp(rb.DenseDist(d_total, m), rb.RNGState(0))
+    lda = m + args.lda_pad
+    if args.lda_pad and kind in ("dense", "saso"):
+        Ap = torch.empty(lda * n, dtype=tdt, device=dev)
+        Ap.view(n, lda)[:, :m].copy_(A.view(n, m))
+        A = Ap
+        del Ap
+    if kind in ("sksy", "sksyp"):   # A symmetric: A := (A + A^T) / 2 (input prep, not timed)
+        Am = A.view(n, m)
+        A.copy_(((Am + Am.t()) * 0.5).reshape(-1))
+        del Am
+    if kind == "sksyp":   # BLAS packed upper triangle, ColMajor: column j's A(0..j, j) in turn
+        Av = A.view(n, m)   # row j of the view = column j of A
+        A = Av.masked_select(torch.ones(n, n, dtype=torch.bool, device=dev).tril()).contiguous()
+        del Av
+        torch.cuda.empty_cache()
+
+    # One library call per step. Nothing is recorded around it here: the only events in the timed
+    # steps are the library's own around its dominant kernel (kernel_ms); every further event
+    # record adds its packet to the measured step.
+    def compute(ro_s, j0, j1, out):
+        """This rank's shard of B = S A over columns j0 .. j1 of its A: rows ro_s .. ro_s + d (dense),
+        all d rows (SASO, whose A block is already this rank's columns)."""
+        rb.sketch_general_left("C", "N", "N", d, j1 - j0, m, 1.0, S, A[j0 * lda:], lda, 0.0, out, d, ro_s=ro_s)
+
+    def sksy(ro_s, out):
+        """One sketch_symmetric call (sksy.hh:520-537) with the reference's default sym_check_tol = 0:
+        the device symmetry check, then the sketch on A's full storage (as the reference computes it)."""
+        rb.sketch_symmetric_left("C", d, n, 1.0, S, A, n, 0.0, out, d, ro_s=ro_s, sym_check_tol=0.0)
+
+    def sksyp(ro_s, out):
+        """The packed-symmetric sketch (rbh_sksy_tri, the one-triangle kernel on packed storage)."""
+        rb.sketch_symmetric_tri("C", "L", "U", "P", d, n, 1.0, S, A, 0, 0.0, out, d, ro_s=ro_s)
+
+    drv = None
+    if use_dist and kind == "saso":
+        from randblas_amd.distributed import ColumnShardedSketch
+
+        B_full = torch.empty(d * world * n, dtype=tdt, device=dev)
+        drv = ColumnShardedSketch(d, n, lambda j0, j1, out: compute(0, j0, j1, out), tdt, dev, chunks=args.chunks)
+    elif use_dist:
+        from randblas_amd.distributed import RowShardedSketch
+
+        B_full = torch.empty(d_total * n, dtype=tdt, device=dev)
+        if kind in ("sksy", "sksyp"):   # the symmetric sketch takes the whole square A: one chunk per rank
+            fn = sksy if kind == "sksy" else sksyp
+            drv = RowShardedSketch(d_total, n, lambda ro, j0, j1, out: fn(ro, out), tdt, dev, chunks=1)
+        else:
+            from randblas_amd.distributed import dense_rank_compute
+
+            drv = RowShardedSketch(d_total, n, dense_rank_compute(S, A, lda, m, d, n), tdt, dev, chunks=args.chunks)
+
+    if drv is not None:
+        def step():
+            drv(B_full)
+    else:
+        B = torch.empty(d * n, dtype=tdt, device=dev)
+
+        def step():
+            if kind == "sksy":
+                sksy(0, B)
+            elif kind == "sksyp":
+                sksyp(0, B)
+            else:
+                compute(0, 0, n, B)
+
+    def sync_all():
+        torch.cuda.synchronize()
+        if use_dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def max_over_ranks(x):
+        if not use_dist:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    for _ in range(args.warmup):
+        step()
+    if drv is not None:
+        drv.wait()
+        drv.timing = True   # compute per timed step; the rest of the step time is exchange left exposed
+    sync_all()
+    rb.kernel_timing(True)   # HIP events around each call's dominant kernel, on its launch stream
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if drv is not None:
+        drv.wait()   # the last step's exchange (the earlier ones overlapped the next step's compute)
+    sync_all()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+    comp_ms = drv.compute_ms() if drv is not None else None
+    kt = rb.kernel_times_ms()
+    rb.kernel_timing(False)
+    single_ms = None
+    if drv is not None:   # single-call latency: one step alone, its whole exchange included
+        drv.timing = False
+        sync_all()
+        t1 = time.perf_counter()
+        step()
+        drv.wait()
+        sync_all()
+        single_ms = max_over_ranks(time.perf_counter() - t1) * 1e3
+    launches = len(kt)
+    kern_ms = float(np.mean(kt))            # average duration of one dominant-kernel launch
+    ms_step = elapsed * 1e3 / args.steps
+    cols_per_launch = n * args.steps / max(launches, 1)
+    exch_ms = max(0.0, ms_step - comp_ms) if comp_ms is not None else None
+
+    # roofline of the dominant kernel: algorithmic work of one launch / its average duration (the
+    # sharded drivers run their chunks one after another on the compute stream, so a launch's
+    # events time that launch alone)
+    esz = 8 if dtype == "f64" else 4
+    t_s = kern_ms * 1e-3
+    if kind == "saso":
+        alg = (m * cols_per_launch + d * cols_per_launch) * esz   # read A panel once, write B once
+        achieved = alg / t_s
+        roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK, "traffic": None, "algorithmic_bytes": alg}
+    else:
+        flops = 2.0 * d * m * cols_per_launch
+        achieved = flops / t_s
+        roof = {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK[dtype] / 1e12, "unit": "TFLOP/s",
+                "frac": achieved / PEAK[dtype], "traffic": None, "algorithmic_flops": flops}
+    roof["basis"] = "kernel"
+    roof["traffic"], roof["traffic_source"] = pmc_traffic(config)
+
+    # the kernel the dense paths ran (sksy: the sketch on A's full storage, the same plan)
+    plan, kname = None, None
+    if kind in ("dense", "sksy"):
+        pl = rb.plan_left("C", "N", "N", d, n, m, S, A, n if kind == "sksy" else lda, d,
+                          ro_s=rank * d if use_dist else 0, dtype=dtype)
+        plan = {"kernel": pl.kernel, "splitk": pl.splitk, "tiles": pl.tiles, "workgroups": pl.workgroups}
+        kname = KERNEL_NAMES.get(pl.kernel, pl.kernel)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and cpu_target_s > 0:
+        try:
+            cpu = cpu_baseline(kind, dtype, d, m, n, vec_nnz, target_s=cpu_target_s)
+        except Exception as e:  # the baseline never blocks the GPU line
+            log(f"cpu_baseline failed: {e!r}")
+
+    return {
+        # d x (world n) entries for SASO, d_total x n dense
+        "value": (world * d * n if kind == "saso" else d_total * n) / (ms_step * 1e-3),
+        "unit": "sketched entries/s",
+        "ms_per_step": ms_step,
+        "kernel_ms": kern_ms,
+        "kernel_launches_per_step": launches / args.steps,
+        # sharded runs: the compute of a step, and the rest of the step time: the all-gather +
+        # unpack not hidden under the next step's compute; and one step timed alone
+        "compute_ms_per_step": comp_ms,
+        "exposed_exchange_ms_per_step": exch_ms,
+        "single_call_ms": single_ms,
+        "scaling": scaling,
+        "dtype": dtype,
+        "data": ("synthetic (A ~ Gaussian DenseDist(m,n) key 99 generated on device; "
+                 + (("the SASO operator filled once before timing, applied from its arrays)" if prefilled
+                     else "the SASO operator sampled in every call)") if kind == "saso" else
+                    "the operator window drawn on the device in every call)")),
+        "config": {"workload": WORKLOADS[config] + (", operator filled once" if prefilled else ""),
+                   "d": d if kind == "saso" else d_total, "d_per_gpu": d, "m": m,
+                   "n": world * n if kind == "saso" else n, "n_per_gpu": n, "layout": "ColMajor",
+                   "operator": "SparseSkOp SASO" if kind == "saso" else "DenseSkOp Gaussian MajorAxis::Long",
+                   "symmetry_check": ("tol=0, timed in the step" if kind == "sksy" else None),
+                   "A_storage": {"sksy": "full", "sksyp": "packed upper (n(n+1)/2)"}.get(kind, "full"),
+                   "parallelism": (f"{'column' if kind == 'saso' else 'row'}-shard x{world} + RCCL all-gather"
+                                   if use_dist else "single GPU")},
+        "pct_of_peak": roof["frac"] * 100.0,
+        # what kernel_ms and the roofline time; any other launch of the step is in ms_per_step only
+        "dominant_kernel": {"dense": f"{kname} (one per chunk)",
+                            "saso": "saso_dma_kernel (sampling and the CSR build: ms_per_step only)",
+                            "sksy": f"{kname} (the symmetry check, the step's other launch: ms_per_step only)",
+                            "sksyp": "skge_wide_kernel<TRI 3>"}[kind],
+        # the library's plan of the dense rank problem (rbh_lskge3_plan): kernel, split-K, tiles
+        "plan": plan,
+        "roofline": roof,
+        "cpu_baseline": cpu,
+    }
 
 
 def main():
@@ -221,7 +446,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                    help="time this config alone (default: the headline c2, then every other BASELINE config "
+                         "as sub-records of the same line)")
+    ap.add_argument("--no-configs", action="store_true", help="the headline config only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--chunks", type=int, default=1,
                     help="column chunks per rank and step, each all-gathered as soon as it is done (N > 1 or --dist; "
@@ -237,7 +465,13 @@ def main():
                          "every step, the reference's fill-once / apply-many use; default: sampled in every call")
     ap.add_argument("--split-d", action="store_true",
                     help="fixed problem (strong scaling): the config's total d split over the ranks (ro_s = g d / N)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="CPU work per baseline sample of the headline config (sub-configs: a third of it)")
     args = ap.parse_args()
+    headline = args.config or "c2"
+    subs = [] if (args.config or args.no_configs) else SUB_CONFIGS
+    if args.split_d:   # strong scaling applies to the dense configs only
+        subs = [sc for sc in subs if CONFIGS[sc[1]][0] != "saso"]
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(relaunch(args.gpus))
@@ -248,7 +482,7 @@ def main():
         log(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}")
         sys.exit(2)
     if args.dry_run:
-        dry_run(args, world, rank)
+        dry_run(args, world, rank, headline, subs)
         return
     use_dist = world > 1 or args.dist
     if use_dist:
@@ -261,215 +495,25 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    kind, dtype, d, m, n, vec_nnz = CONFIGS[args.config]
-    d_total, d, scaling = shard_rows(args, world)   # d: this rank's rows (dense) / all rows (SASO)
-    tdt = torch.float64 if dtype == "f64" else torch.float32
-
-    # A ~ DenseDist(m, n) Gaussian key 99, ColMajor, generated on the device (input, not timed).
-    # SASO shards by columns: rank g holds columns [g n, (g+1) n) of DenseDist(m, world n).
-    A = torch.empty(m * n, dtype=tdt, device=dev)
-    if kind == "saso":
-        rb.fill_dense("C", rb.DenseDist(m, world * n), m, n, 0, rank * n, A, rb.RNGState(99))
-        S = rb.SparseSkOp(rb.SparseDist(d, m, vec_nnz), rb.RNGState(0))
-        if args.prefilled:   # fill once (untimed), apply from the arrays every step (skge.hh:503-504)
-            rb.fill_sparse_op(S)
-    else:
-        rb.fill_dense("C", rb.DenseDist(m, n), m, n, 0, 0, A, rb.RNGState(99))
-        S = rb.DenseSkOp(rb.DenseDist(d_total, m), rb.RNGState(0))
-    lda = m + args.lda_pad
-    if args.lda_pad and kind == "dense":
-        Ap = torch.empty(lda * n, dtype=tdt, device=dev)
-        Ap.view(n, lda)[:, :m].copy_(A.view(n, m))
-        A = Ap
-        del Ap
-    if kind in ("sksy", "sksyp"):   # A symmetric: A := (A + A^T) / 2 (input prep, not timed)
-        Am = A.view(n, m)
-        A.copy_(((Am + Am.t()) * 0.5).reshape(-1))
-        del Am
-    if kind == "sksyp":   # BLAS packed upper triangle, ColMajor: column j's A(0..j, j) in turn
-        Av = A.view(n, m)   # row j of the view = column j of A
-        A = Av.masked_select(torch.ones(n, n, dtype=torch.bool, device=dev).tril()).contiguous()
-        del Av
-        torch.cuda.empty_cache()
-
-    def timed(fn, record):
-        """One library call. Nothing is recorded around it here: the only events in the timed steps
-        are the library's own around its dominant kernel (kernel_ms); every further event record
-        adds its packet to the measured step."""
-        fn()
-
-    def compute(ro_s, j0, j1, out, record=False):
-        """This rank's shard of B = S A over columns j0 .. j1 of its A: rows ro_s .. ro_s + d (dense),
-        all d rows (SASO, whose A block is already this rank's columns)."""
-        Ach = A[j0 * lda:]
-        timed(lambda: rb.sketch_general_left("C", "N", "N", d, j1 - j0, m, 1.0, S, Ach, lda, 0.0, out, d, ro_s=ro_s),
-              record)
-
-    def sksy(ro_s, out, record=False):
-        """One sketch_symmetric call (sksy.hh:520-537) with the reference's default sym_check_tol = 0:
-        the device symmetry check, then the sketch on A's full storage (as the reference computes it)."""
-        timed(lambda: rb.sketch_symmetric_left("C", d, n, 1.0, S, A, n, 0.0, out, d, ro_s=ro_s, sym_check_tol=0.0),
-              record)
-
-    def sksyp(ro_s, out, record=False):
-        """The packed-symmetric sketch (rbh_sksy_tri, the one-triangle kernel on packed storage)."""
-        timed(lambda: rb.sketch_symmetric_tri("C", "L", "U", "P", d, n, 1.0, S, A, 0, 0.0, out, d, ro_s=ro_s), record)
-
-    recording = [False]
-    if use_dist and kind == "saso":
-        from randblas_amd.distributed import ColumnShardedSketch
-
-        B_full = torch.empty(d * world * n, dtype=tdt, device=dev)
-        drv = ColumnShardedSketch(d, n, lambda j0, j1, out: compute(0, j0, j1, out, recording[0]), tdt, dev,
-                                  chunks=args.chunks)
-
-        def step(record=False):
-            recording[0] = record
-            drv(B_full)
-    elif use_dist:
-        from randblas_amd.distributed import RowShardedSketch
-
-        B_full = torch.empty(d_total * n, dtype=tdt, device=dev)
-        if kind in ("sksy", "sksyp"):   # the symmetric sketch takes the whole square A: one chunk per rank
-            fn = sksy if kind == "sksy" else sksyp
-            drv = RowShardedSketch(d_total, n, lambda ro, j0, j1, out: fn(ro, out, recording[0]), tdt, dev,
-                                   chunks=1)
-        else:
-            from randblas_amd.distributed import dense_rank_compute
-
-            drv = RowShardedSketch(d_total, n, dense_rank_compute(S, A, lda, m, d, n), tdt, dev, chunks=args.chunks)
-
-        def step(record=False):
-            recording[0] = record
-            drv(B_full)
-    else:
-        B = torch.empty(d * n, dtype=tdt, device=dev)
-
-        def step(record=False):
-            if kind == "sksy":
-                sksy(0, B, record)
-            elif kind == "sksyp":
-                sksyp(0, B, record)
-            else:
-                compute(0, 0, n, B, record)
-
-    for _ in range(args.warmup):
-        step()
-    if use_dist:
-        drv.timing = True   # compute per timed step; the rest of the step time is exchange left exposed
-    torch.cuda.synchronize()
-    if use_dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    rb.kernel_timing(True)   # HIP events around each call's dominant kernel, on its launch stream
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(record=True)
-    if use_dist:
-        drv.wait()   # the last step's exchange (the earlier ones overlapped the next step's compute)
-    torch.cuda.synchronize()
-    if use_dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if use_dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    comp_ms = drv.compute_ms() if use_dist else None
-    kt = rb.kernel_times_ms()
-    rb.kernel_timing(False)
-    launches = len(kt)
-    kern_ms = float(np.mean(kt))            # average duration of one dominant-kernel launch
-    ms_step = elapsed * 1e3 / args.steps
-    cols_per_launch = n * args.steps / max(launches, 1)
-
-    exch_ms = max(0.0, ms_step - comp_ms) if comp_ms is not None else None
-    # roofline of the dominant kernel: algorithmic work of one launch / its average duration (the
-    # sharded drivers run their chunks one after another on the compute stream, so a launch's
-    # events time that launch alone)
-    esz = 8 if dtype == "f64" else 4
-    per = "kernel"
-    t_s = kern_ms * 1e-3
-    if kind == "saso":
-        alg = (m * cols_per_launch + d * cols_per_launch) * esz   # read A panel once, write B once
-        achieved = alg / t_s
-        roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK, "traffic": None}
-    else:
-        flops = 2.0 * d * m * cols_per_launch
-        achieved = flops / t_s
-        roof = {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK[dtype] / 1e12, "unit": "TFLOP/s",
-                "frac": achieved / PEAK[dtype], "traffic": None}
-
-    roof["basis"] = per
-    roof["traffic"], roof["traffic_source"] = pmc_traffic(args.config)
-
-    # the kernel the dense paths ran (sksy: the sketch on A's full storage, the same plan)
-    plan, kname = None, None
-    if kind in ("dense", "sksy"):
-        pl = rb.plan_left("C", "N", "N", d, n, m, S, A, n if kind == "sksy" else lda, d,
-                          ro_s=rank * d if use_dist else 0, dtype=dtype)
-        plan = {"kernel": pl.kernel, "splitk": pl.splitk, "tiles": pl.tiles, "workgroups": pl.workgroups}
-        kname = KERNEL_NAMES.get(pl.kernel, pl.kernel)
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    head = run_config(args, headline, args.prefilled, world, rank, dev, use_dist, args.cpu_seconds)
+    sub = {}
+    for name, cfg, pre in subs:
         try:
-            cpu = cpu_baseline(kind, dtype, d, m, n, vec_nnz)
-        except Exception as e:  # the baseline never blocks the GPU line
-            log(f"cpu_baseline failed: {e!r}")
+            sub[name] = run_config(args, cfg, pre, world, rank, dev, use_dist, args.cpu_seconds / 3.0)
+        except Exception as e:  # a failing sub-config never loses the headline line
+            log(f"bench: config {name} failed: {e!r}")
+            sub[name] = {"error": repr(e)}
+            torch.cuda.empty_cache()
 
     if rank == 0:
-        line = {
-            "metric": "sketched-entries/sec (d*n/s) + achieved-%-of-fp64-MFMA-peak, skge d x m * m x n",
-            # d x (world n) entries for SASO, d_total x n dense
-            "value": (world * d * n if kind == "saso" else d_total * n) / (ms_step * 1e-3),
-            "unit": "sketched entries/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_step,
-            "kernel_ms": kern_ms,
-            "kernel_launches_per_step": launches / args.steps,
-            # sharded runs (rank 0): the compute of a step, and the rest of the step time: the
-            # all-gather + unpack not hidden under the next step's compute
-            "compute_ms_per_step": comp_ms,
-            "exposed_exchange_ms_per_step": exch_ms,
-            "higher_is_better": True,
-            "scaling": scaling,
-            "vs_baseline": None,
-            "dtype": dtype,
-            "data": ("synthetic (A ~ Gaussian DenseDist(m,n) key 99 generated on device; "
-                     + (("the SASO operator filled once before timing, applied from its arrays)" if args.prefilled
-                         else "the SASO operator sampled in every call)") if kind == "saso" else
-                        "the operator window drawn on the device in every call)")),
-            "config": {"workload": {"c1": "Gaussian skge fp64 d=128 A 4096^2 (BASELINE configs[0], the reference's CPU case)",
-                                    "c2": "Gaussian skge fp64 (BASELINE configs[1])",
-                                    "ns": "Gaussian skge fp64 north-star",
-                                    "c3": "SASO SparseSkOp vec_nnz=8 fp64 (configs[2])",
-                                    "c4": "Gaussian skge fp32 (configs[3])",
-                                    "c5": "sksy fp64, sketch_symmetric with sym_check_tol=0 (configs[4])",
-                                    "c5p": "sksy fp64 on packed-symmetric A (configs[4] as worded)"}[args.config],
-                       "d": d if kind == "saso" else d_total, "d_per_gpu": d, "m": m,
-                       "n": world * n if kind == "saso" else n, "n_per_gpu": n, "layout": "ColMajor",
-                       "operator": "SparseSkOp SASO" if kind == "saso" else "DenseSkOp Gaussian MajorAxis::Long",
-                       "symmetry_check": ("tol=0, timed in the step" if kind == "sksy" else None),
-                       "A_storage": {"sksy": "full", "sksyp": "packed upper (n(n+1)/2)"}.get(kind, "full"),
-                       "parallelism": (f"{'column' if kind == 'saso' else 'row'}-shard x{world} + RCCL all-gather"
-                                       if use_dist else "single GPU")},
-            "pct_of_peak": roof["frac"] * 100.0,
-            # what kernel_ms and the roofline time; any other launch of the step is in ms_per_step only
-            "dominant_kernel": {"dense": f"{kname} (one per chunk)",
-                                "saso": "saso_dma_kernel (sampling and the CSR build: ms_per_step only)",
-                                "sksy": f"{kname} (the symmetry check, the step's other launch: "
-                                        "ms_per_step only)",
-                                "sksyp": "skge_wide_kernel<TRI 3>"}[kind],
-            # the library's plan of the dense rank problem (rbh_lskge3_plan): kernel, split-K, tiles
-            "plan": plan,
-            "roofline": roof,
-            "cpu_baseline": cpu,
-        }
+        line = {"metric": "sketched-entries/sec (d*n/s) + achieved-%-of-fp64-MFMA-peak, skge d x m * m x n",
+                "value": head.pop("value"), "unit": head.pop("unit"), "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": head.pop("ms_per_step"), "higher_is_better": True,
+                "scaling": head.pop("scaling"), "vs_baseline": None}
+        line.update(head)
+        if sub:
+            # every other BASELINE config, timed in this same process with the same steps and warm-up
+            line["configs"] = sub
         print(json.dumps(line), flush=True)
     if use_dist:
         dist.destroy_process_group()

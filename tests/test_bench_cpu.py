@@ -46,3 +46,29 @@ def test_bench_weak_scaling_default():
     assert r.returncode == 0, r.stderr[-2000:]
     line = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")][0]
     assert line["d"] == 2048 and line["d_per_gpu"] == 1024 and line["scaling"] == "weak"
+
+
+def test_bench_default_times_every_config():
+    """A default run times the headline (c2) and then every other BASELINE config in the same process:
+    the dry run lists them (NS, C3 sampled and pre-filled, C4, C5, C5p, C1); --config X times X alone."""
+    r = _run(["--dry-run", "--steps", "1", "--warmup", "0"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")][0]
+    assert line["config"] == "c2"
+    assert line["configs"] == ["ns", "c3", "c3_prefilled", "c4", "c5", "c5p", "c1"]
+    r = _run(["--dry-run", "--config", "c4", "--steps", "1", "--warmup", "0"])
+    line = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")][0]
+    assert line["config"] == "c4" and line["configs"] == []
+
+
+def test_trace_frac_recomputes_a_committed_trace():
+    """tools/trace_frac.py: a committed per-launch kernel trace gives the config's roofline fraction
+    from its steady launches (warm-ups dropped)."""
+    import glob
+    traces = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "c2_kernel_trace.csv")))
+    assert traces
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "trace_frac.py"), "c2", traces[-1], "--warmup", "2",
+                        "--json"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    res = json.loads(r.stdout)
+    assert res["steady"] >= 1 and 0.3 < res["frac"] < 1.0

@@ -26,6 +26,7 @@ case " $what " in *" tests "*)
     run smoke.log 300 python -u -c "import __graft_entry__ as g; g.smoke()"
 ;; esac
 case " $what " in *" bench "*)
+    run bench_all.log 600 python -u bench.py
     for c in $CONFIGS; do run "bench_$c.log" 300 python -u bench.py --config "$c"; done
     run bench_c3pre.log 300 python -u bench.py --config c3 --prefilled
     for c in ${DIST_CONFIGS:-c2 ns c3 c4}; do
@@ -33,11 +34,19 @@ case " $what " in *" bench "*)
     done
 ;; esac
 case " $what " in *" prof "*)
+    # per-launch traces: 20 timed steps after 3 warm-ups, so tools/trace_frac.py recomputes each
+    # config's frac from >= 10 steady launches
     for c in $CONFIGS; do
         run "rocprof_$c.log" 300 rocprofv3 --kernel-trace --stats -d "gpurun_out/prof_$c" -o run \
-            --output-format csv -- python3 bench.py --config "$c" --steps 5 --warmup 2 --no-cpu-baseline
+            --output-format csv -- python3 bench.py --config "$c" --steps 20 --warmup 3 --no-cpu-baseline
         f=$(find "gpurun_out/prof_$c" -name "*kernel_stats.csv" | head -n 1)
         [ -n "$f" ] && cp "$f" "gpurun_out/${c}_kernel_stats.csv"
+        f=$(find "gpurun_out/prof_$c" -name "*kernel_trace.csv" | head -n 1)
+        if [ -n "$f" ]; then
+            cp "$f" "gpurun_out/${c}_kernel_trace.csv"
+            python3 tools/trace_frac.py "$c" "gpurun_out/${c}_kernel_trace.csv" --warmup 3 --json \
+                > "gpurun_out/${c}_trace_frac.json" || true
+        fi
     done
 ;; esac
 case " $what " in *" pmc "*)
