@@ -1086,6 +1086,103 @@ template <> hipError_t launch_sym_t<float>(char l, const float *A, int64_t n, in
     return launch_symcheck_f32(l, A, n, lda, tol, f, s);
 }
 
+template <typename T> hipError_t launch_sym_lean_t(char, const T *, int64_t, int64_t, T, int *, hipStream_t);
+template <> hipError_t launch_sym_lean_t<double>(char l, const double *A, int64_t n, int64_t lda, double tol, int *f,
+                                                 hipStream_t s) {
+    return launch_symcheck_lean_f64(l, A, n, lda, tol, f, s);
+}
+template <> hipError_t launch_sym_lean_t<float>(char l, const float *A, int64_t n, int64_t lda, float tol, int *f,
+                                                hipStream_t s) {
+    return launch_symcheck_lean_f32(l, A, n, lda, tol, f, s);
+}
+template <typename T> hipError_t launch_commit_t(int64_t, int64_t, const T *, T, T *, int64_t, const int *, hipStream_t);
+template <> hipError_t launch_commit_t<double>(int64_t M, int64_t N, const double *W, double b, double *C, int64_t ldc,
+                                               const int *f, hipStream_t s) {
+    return launch_sksy_commit_f64(M, N, W, b, C, ldc, f, s);
+}
+template <> hipError_t launch_commit_t<float>(int64_t M, int64_t N, const float *W, float b, float *C, int64_t ldc,
+                                              const int *f, hipStream_t s) {
+    return launch_sksy_commit_f32(M, N, W, b, C, ldc, f, s);
+}
+
+// The library's side stream of the current device (non-blocking, made once) and a thread's pair of
+// fork / join events on it: sketch_symmetric runs its symmetry check there, beside the sketch.
+hipError_t side_stream(hipStream_t *out, hipEvent_t *fork, hipEvent_t *join) {
+    static std::mutex mu;
+    static std::map<int, hipStream_t> streams;
+    thread_local std::map<int, std::pair<hipEvent_t, hipEvent_t>> events;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = streams.find(dev);
+        if (it == streams.end()) {
+            hipStream_t st = nullptr;
+            e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+            if (e != hipSuccess) return e;
+            it = streams.emplace(dev, st).first;
+        }
+        *out = it->second;
+    }
+    auto ev = events.find(dev);
+    if (ev == events.end()) {
+        hipEvent_t a = nullptr, b = nullptr;
+        e = hipEventCreateWithFlags(&a, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&b, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+        ev = events.emplace(dev, std::make_pair(a, b)).first;
+    }
+    *fork = ev->second.first;
+    *join = ev->second.second;
+    return hipSuccess;
+}
+
+// sketch_symmetric's check and sketch at once (the full-storage path): the GEMM computes alpha S A
+// into a workspace W on the caller's stream while the low-register check (symcheck_lean_kernel, which
+// fits beside the GEMM's waves) reads A on the side stream; after both, a commit kernel writes
+// C = W + beta C unless the check failed, so C keeps the GEMM's bits and stays untouched on failure,
+// as when the reference throws before sketching. Returns RBH_OK with *flags set (the call waits for
+// them), or a HIP failure; *done = false when the workspace could not be had (nothing launched).
+template <typename T>
+int sksy_overlapped(GemmProblem p, char layout, const T *dA, int64_t n, int64_t lda, T tol, hipStream_t s, int *flags,
+                    bool *done) {
+    *done = false;
+    *flags = 0;
+    if (p.M <= 0 || p.N <= 0 || p.K <= 0 || p.alpha == 0.0) return RBH_OK;
+    hipStream_t s2;
+    hipEvent_t fork, join;
+    RBH_HIP(side_stream(&s2, &fork, &join));
+    int *flag = nullptr;
+    T *W = nullptr;
+    if (ws_alloc((void **)&flag, sizeof(int), s) != hipSuccess) { (void)hipGetLastError(); return RBH_OK; }
+    if (ws_alloc((void **)&W, sizeof(T) * (size_t)p.M * (size_t)p.N, s) != hipSuccess) {
+        (void)hipGetLastError();
+        RBH_HIP(ws_free(flag, s));
+        return RBH_OK;
+    }
+    *done = true;
+    T *C = (T *)p.C;
+    const int64_t ldc = p.ldc;
+    const T beta = (T)p.beta;
+    p.C = W;
+    p.ldc = p.M;
+    p.beta = 0.0;
+    RBH_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
+    RBH_HIP(hipEventRecord(fork, s));
+    RBH_HIP(launch_gemm_t<T>(p, s));           // the sketch first: its workgroups take the CUs
+    RBH_HIP(hipStreamWaitEvent(s2, fork, 0));
+    RBH_HIP(launch_sym_lean_t<T>(layout, dA, n, lda, tol, flag, s2));
+    RBH_HIP(hipEventRecord(join, s2));
+    RBH_HIP(hipStreamWaitEvent(s, join, 0));
+    RBH_HIP(launch_commit_t<T>(p.M, p.N, W, beta, C, ldc, flag, s));
+    RBH_HIP(hipMemcpyAsync(flags, flag, sizeof(int), hipMemcpyDeviceToHost, s));
+    RBH_HIP(ws_free(W, s));
+    RBH_HIP(ws_free(flag, s));
+    RBH_HIP(hipStreamSynchronize(s));
+    return RBH_OK;
+}
+
 // The device check on a device pointer: *flags bit 0 = the reference's predicate failed somewhere,
 // bit 1 = some mirrored pair is not bitwise equal. Synchronises the stream (the caller must know).
 template <typename T>
@@ -1242,6 +1339,27 @@ int sketch_symmetric(char layout, char side, int64_t d, int64_t n, T alpha, cons
     void *dA, *dB, *dS;
     RBH_HIP(st.map(A, sizeof(T) * extent(layout, n, n, lda), true, false, &dA));
     int flags = 2;   // unchecked: read both triangles
+    const bool use_tri = opt && opt->sksy_triangle;
+    if (tol >= 0 && !use_tri) {
+        // the default (full storage): check and sketch at once, the result committed if the check passed
+        RBH_HIP(st.map_out(B, sizeof(T), layout, side == 'L' ? d : n, side == 'L' ? n : d, ldb, beta != (T)0, &dB));
+        RBH_HIP(st.map(S_buff, sizeof(T) * D->n_rows * D->n_cols, true, false, &dS));
+        GemmProblem p{};
+        if (side == 'L') build_left<T>(p, layout, 'N', 'N', d, n, n, alpha, beta, D, seed, dS, S_layout, ro_s, co_s,
+                                       dA, lda, dB, ldb);
+        else build_right<T>(p, layout, 'N', 'N', n, d, n, alpha, beta, dA, lda, D, seed, dS, S_layout, ro_s, co_s, dB,
+                            ldb);
+        apply_options(p, opt);
+        bool done = false;
+        rc = sksy_overlapped<T>(p, layout, (const T *)dA, n, lda, tol, s, &flags, &done);
+        if (rc) return rc;
+        if (done) {
+            if (flags & 1) return set_error(RBH_ERR_SYMMETRY, "Symmetry check failed, in function require_symmetric");
+            RBH_HIP(st.finish());
+            g_sksy_path = 0;
+            return RBH_OK;
+        }
+    }
     if (tol >= 0) {
         rc = symcheck_flags<T>(layout, (const T *)dA, n, lda, tol, s, &flags);
         if (rc) return rc;
@@ -1249,7 +1367,6 @@ int sketch_symmetric(char layout, char side, int64_t d, int64_t n, T alpha, cons
     }
     RBH_HIP(st.map_out(B, sizeof(T), layout, side == 'L' ? d : n, side == 'L' ? n : d, ldb, beta != (T)0, &dB));
     RBH_HIP(st.map(S_buff, sizeof(T) * D->n_rows * D->n_cols, true, false, &dS));
-    const bool use_tri = opt && opt->sksy_triangle;
     const int path = (!(flags & 2) && use_tri) ? 1 : 0;
     if (path == 1) {
         rc = sksy_tri_dev<T>(layout, side, 'U', 'F', d, n, alpha, D, seed, dS, S_layout, ro_s, co_s, dA, lda, beta,

@@ -25,6 +25,7 @@
 //      The dense operand is read from HBM once per 16-column panel; no atomics, deterministic.
 #include "common.hpp"
 #include "saso.hpp"
+#include "variants.hpp"
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
@@ -912,29 +913,14 @@ __global__ __launch_bounds__(SU_NT) void saso_unit_kernel(const SparseApply p, c
 //    instead of the barrier, a rotating or dedicated copy wave, copies interleaved with the walk,
 //    an L2 prefetch of the panel after next.
 // ------------------------------------------------------------------------------------------
-#ifndef SD_KCS_DEF
-#define SD_KCS_DEF 7
-#endif
-#ifndef SD_NB_DEF
-#define SD_NB_DEF 2
-#endif
-#ifndef SD_PD_DEF
-#define SD_PD_DEF 1
-#endif
 constexpr int SD_KCS = SD_KCS_DEF;   // log2 of the chunk depth
 constexpr int SD_KC = 1 << SD_KCS;   // contracted indices per chunk
 constexpr int SD_NB = SD_NB_DEF;     // panel buffers (a ring)
 constexpr int SD_PD = SD_PD_DEF;     // panels in flight ahead of the walked one
 static_assert(SD_NB >= SD_PD + 1 && (SD_NB & (SD_NB - 1)) == 0, "ring: the walked panel plus the ones in flight");
-#ifndef SD_PAD8_DEF
-#define SD_PAD8_DEF 1
-#endif
 // Y along k: SD_PAD8 pads each panel column by 8 B (stride KC * 8 + 8) instead of XOR-swizzling
 // its 16-B slots, so the 32 lanes of a ds_read_b64 lane group hit 64 distinct banks
 constexpr bool SD_PAD8 = SD_PAD8_DEF;
-#ifndef SD_CW_DEF
-#define SD_CW_DEF 4
-#endif
 constexpr int SD_CW = SD_CW_DEF;   // waves that issue the panel copies (the first SD_CW)
 constexpr int SD_BR = 8;             // record-bound ring slots (chunks c + 1 .. c + SD_PD + 1 live)
 static_assert(SD_BR >= SD_PD + 2, "bounds ring");

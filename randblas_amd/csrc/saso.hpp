@@ -60,5 +60,15 @@ hipError_t launch_symcheck_f64(char layout, const double *A, int64_t n, int64_t 
                                hipStream_t s);
 hipError_t launch_symcheck_f32(char layout, const float *A, int64_t n, int64_t lda, float tol, int *flag,
                                hipStream_t s);
+// the low-register check for running beside the sketch GEMM, and the commit of the GEMM's output
+// (C = W + beta C unless the check failed); sksy.hip
+hipError_t launch_symcheck_lean_f64(char layout, const double *A, int64_t n, int64_t lda, double tol, int *flag,
+                                    hipStream_t s);
+hipError_t launch_symcheck_lean_f32(char layout, const float *A, int64_t n, int64_t lda, float tol, int *flag,
+                                    hipStream_t s);
+hipError_t launch_sksy_commit_f64(int64_t M, int64_t N, const double *W, double beta, double *C, int64_t ldc,
+                                  const int *flag, hipStream_t s);
+hipError_t launch_sksy_commit_f32(int64_t M, int64_t N, const float *W, float beta, float *C, int64_t ldc,
+                                  const int *flag, hipStream_t s);
 
 }  // namespace rbh

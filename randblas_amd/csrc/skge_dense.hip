@@ -23,6 +23,7 @@
 //   * Tiles are numbered output-row-fastest and dealt XCD-contiguously (bijective remap), so the
 //     row tiles that share one Y column panel run on one XCD and share its L2.
 #include "common.hpp"
+#include "variants.hpp"
 
 #include <type_traits>
 
@@ -1176,12 +1177,6 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
 //    round, so the draw is spread evenly over the four SIMDs and the waves meet once per round.
 // Requires K % (128 / sizeof(T)) == 0, a memory operand with 16-B aligned rows contiguous along k
 // (mode 2), pc0 % 4 == 0, and the wave's 128 rows addressable with 32-bit byte offsets.
-#ifndef RBH_STREAM_ZMAJOR
-#define RBH_STREAM_ZMAJOR 0
-#endif
-#ifndef RBH_STREAM_PARTS64
-#define RBH_STREAM_PARTS64 2   // f64 64 x 512: a step in two 16-B parts (variant builds: 1)
-#endif
 // Block-major part order (both 16-B halves of a lane's 32 B of a row's line loaded back to back). With
 // part-major order the second half was requested half a step after the first, and at a row stride of
 // 128 KiB (f32, m = 32768: every row of a step on the same L2 sets) the line was often gone by then:
@@ -1189,20 +1184,11 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
 // kernel 4.50 -> 4.40 ms (same box, two alternations; profiles/r04/fetch_c4_order.txt). With the
 // scheduling barriers below: f32 the same time in either order with half the L2-miss bytes
 // block-major; f64 0.4 % faster block-major (before the barriers it measured 0.8 % slower).
-#ifndef RBH_STREAM_CMAJOR32
-#define RBH_STREAM_CMAJOR32 1
-#endif
-#ifndef RBH_STREAM_CMAJOR64
-#define RBH_STREAM_CMAJOR64 1
-#endif
 // A scheduling barrier after each prefetch load: with the buffer resource in SGPRs (no waterfall
 // loop around each load any more) the scheduler sank every f32 load to its MFMAs and waited on it at
 // once. f32: C4 4.37 -> 4.03 ms (80.0 -> 86.7 % of the f32 peak, same box, two alternations), L2-miss
 // bytes 9.3-9.7 -> 4.7 GB per launch; d = 1024, m = n = 16384: 74.5 -> 80.5 %. f64 (block-major):
 // C2 8.005-8.011 -> 7.976 ms (profiles/r04/ab_sched_barrier.txt).
-#ifndef RBH_STREAM_SB64
-#define RBH_STREAM_SB64 1
-#endif
 template <typename T, int GK, int FAMILY, bool GX, bool SPLIT, int PF, int BG, int MW, int TRI = 0>
 __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     constexpr int KS = 128 / (int)sizeof(T);              // k per step
@@ -1217,7 +1203,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     constexpr int WCALLS = R / SPU;                       // wave-calls per wave and round (f64 1, f32 4)
     // a step runs in NPART parts: BG = 64 in two (each the lane's next 16 B: half the fragment
     // registers, for the 128 accumulators), BG = 32 in one (the lane's 32 B)
-    constexpr int NPART = BG == 64 ? (sizeof(T) == 8 ? RBH_STREAM_PARTS64 : 2) : 1;
+    constexpr int NPART = BG == 64 ? 2 : 1;
     constexpr int PV = VPL / NPART;                       // values per lane and part
     constexpr int NLD = 2 / NPART;                        // 16-B loads per part fragment
     constexpr int NH = NPART * FB;                        // part-blocks of a step (part FB + c)
@@ -1228,7 +1214,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     // k order either way (its block's parts in turn), so the sums are the same bits
     // (not for the f32 GEN_OO form with the generated operand as Y: it sits near 256 registers and
     // the second part's fragments would spill)
-    constexpr bool CMAJOR = NPART > 1 && (sizeof(T) == 8 ? RBH_STREAM_CMAJOR64 : RBH_STREAM_CMAJOR32) &&
+    constexpr bool CMAJOR = NPART > 1 &&
                             !(sizeof(T) == 4 && GK == GEN_OO && !GX) && !TRI;   // (one-triangle: as measured)
     // part-block (p FB + c, mload's numbering) consumed s-th in block-major order
     auto seq_block = [](int s) -> int { return (s % NPART) * FB + s / NPART; };
@@ -1256,11 +1242,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     const int64_t b = blockIdx.x;
     const int64_t xcd = b % 8, qq = nb / 8, rr = nb % 8;
     const int64_t t_all = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + b / 8;
-#if RBH_STREAM_ZMAJOR
-    const int64_t z = t_all / (nTg * nTm), t = t_all % (nTg * nTm);   // (variant: each split on its own XCDs)
-#else
     const int64_t z = t_all % split, t = t_all / split;
-#endif
     // consecutive tiles share a memory tile (the generated tiles of one memory tile run on one XCD)
     const int64_t go0 = (t % nTg) * BG, mo0 = (t / nTg) * (8 * BMW);
     const int64_t wm0 = mo0 + (int64_t)wave * BMW;        // this wave's first memory row
@@ -1477,7 +1459,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
                         mload(sn % NSLOT, seq_block(sn % NH), ktn);
                         // keep the load here, PF part-blocks ahead of its use (the scheduler otherwise
                         // sinks it next to its MFMAs and waits on it at once)
-                        if (sizeof(T) == 4 || RBH_STREAM_SB64) __builtin_amdgcn_sched_barrier(0);
+                        __builtin_amdgcn_sched_barrier(0);
                         const hv_t &m = mv[s % NSLOT];
 #pragma unroll
                         for (int e = 0; e < PV; ++e)
@@ -1498,7 +1480,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
                     const int i = h * FB + c, in = i + PF;
                     const int64_t ktn = in < NH ? kt : (kt + 1 < kt1 ? kt + 1 : kt);
                     mload(in % NSLOT, in % NH, ktn);
-                    if (sizeof(T) == 4 || RBH_STREAM_SB64) __builtin_amdgcn_sched_barrier(0);   // (as above)
+                    __builtin_amdgcn_sched_barrier(0);   // (as above)
                     const hv_t &m = mv[i % NSLOT];
 #pragma unroll
                     for (int e = 0; e < PV; ++e)
@@ -1730,9 +1712,6 @@ static hipError_t materialise(const GemmProblem &p, void **buf, hipStream_t s) {
     return e;
 }
 
-#ifndef RBH_STREAM_F64_BG32
-#define RBH_STREAM_F64_BG32 1
-#endif
 struct StreamGeom {
     int bg;      // generated rows per tile
     int mw;      // memory rows per wave (the tile's memory rows: 8 mw)
@@ -1802,9 +1781,6 @@ static bool wide_ok(const GemmProblem &p) {
 
 // f32 streamed tile height: 64 (64 x 1024 tiles, 128 accumulator registers) where stream_geom picks
 // it; 32 forces the 32 x 1024 tiles everywhere (variant builds for A/B timing)
-#ifndef RBH_STREAM_BG32
-#define RBH_STREAM_BG32 64
-#endif
 // Streamed-kernel geometry: the generated tile height BG and the split-K factor, which the f32
 // materialised path (skge_wide32_kernel) shares so that both give the same bits. f64: BG = 32, the
 // split of the 64 x 512 kernels. f32: BG = 64 (every loaded memory value feeds four MFMA tiles;
@@ -1825,14 +1801,13 @@ static StreamGeom stream_geom(const GemmProblem &p) {
         // a small grid (split-K 8 or more over 64 x 512 tiles) takes 32 x 512 tiles, half the split:
         // the same workgroups, half the partial sums written and re-read by the reduction (C1:
         // 67 MB -> 34 MB per call)
-        if (RBH_STREAM_F64_BG32 && s32 >= 8 && p.split_req == 0) {
+        if (s32 >= 8 && p.split_req == 0) {
             const int64_t t32 = ((gnO + 31) / 32) * ((mnO + 511) / 512);
             const int sh = choose_split(t32, nk, 0);
             if (sh < s32 && t32 * sh >= wide * s32) return {32, 64, sh};
         }
         return {64, 64, s32};
     }
-    if (RBH_STREAM_BG32 != 64) return {32, 128, s32};
     const int64_t t64 = ((gnO + 63) / 64) * ((mnO + 1023) / 1024), t32 = ((gnO + 31) / 32) * ((mnO + 1023) / 1024);
     const int s64 = choose_split(t64, nk, p.split_req);
     const int64_t cus = device_cus();
@@ -1898,29 +1873,13 @@ static bool wide32_ok(const GemmProblem &p) {
 // f64 streams the wide kernel's own 64 x 512 tiles (C2: 7.99-8.01 ms against 8.72-8.74 ms on
 // skge_wide_kernel, same box, two alternations); f32 streams 64 or 32 x 1024 tiles (stream_geom).
 // The macros exist for variant builds (A/B timing): 0 keeps that type on the 64 x 512 LDS kernels.
-#ifndef RBH_STREAM64
-#define RBH_STREAM64 1
-#endif
-#ifndef RBH_STREAM32
-#define RBH_STREAM32 1
-#endif
 template <typename T>
 static bool stream_ok(const GemmProblem &p) {
-    if (sizeof(T) == 8 ? !RBH_STREAM64 : !RBH_STREAM32) return false;
     return !p.materialise && (sizeof(T) == 8 ? wide_ok<T>(p) : wide32_ok<T>(p));
 }
 
 // part-blocks loaded ahead of their use (a register ring of PF + 1; PF + 1 divides 8)
-#ifndef RBH_STREAM_PF64
-#define RBH_STREAM_PF64 7   // (C2: PF 7 7.99-8.01 ms, PF 3 8.15-8.19 ms)
-#endif
-#ifndef RBH_STREAM_PF32
-#define RBH_STREAM_PF32 3
-#endif
-template <typename T> constexpr int stream_pf() { return sizeof(T) == 8 ? RBH_STREAM_PF64 : RBH_STREAM_PF32; }
-#ifndef RBH_STREAM_PF_TRI
-#define RBH_STREAM_PF_TRI 7   // the one-triangle (f64) instantiations
-#endif
+template <typename T> constexpr int stream_pf() { return sizeof(T) == 8 ? RBH_PF64 : RBH_PF32; }
 
 template <typename T, int GK, int FAMILY, bool GX, int TRI = 0>
 static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
@@ -1939,7 +1898,7 @@ static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
     }
     timing_begin(s);
     const dim3 grid((unsigned)(nb * split));
-    constexpr int PF = TRI ? RBH_STREAM_PF_TRI : stream_pf<T>();
+    constexpr int PF = TRI ? RBH_PF_TRI : stream_pf<T>();
     if constexpr (sizeof(T) == 8) {   // 64 x 512 tiles (64 x 1024 would take 256 accumulator registers)
         if (!TRI && gm.bg == 32) {   // small grids: 32 x 512 tiles (stream_geom), split K
             hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, 3, 32, 64, 0>), grid, dim3(512), 0, s, q);
@@ -1969,14 +1928,11 @@ static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
 // The one-triangle operand stays on skge_wide_kernel by default: streamed, each mirrored step
 // loads 8 B per element (the stored row k holds the lane's row o at a 16-row stride), and C5p
 // measured 4.85 ms against 4.59-4.61 ms through the wide kernel's LDS transpose (same box, two
-// alternations; with PF 3 5.27-5.30 ms). RBH_STREAM_TRI=1 builds stream it (variant A/B timing).
-#ifndef RBH_STREAM_TRI
-#define RBH_STREAM_TRI 0
-#endif
+// alternations; with PF 3 5.27-5.30 ms). RBH_TRI_STREAMED=1 builds stream it (variants.hpp).
 // the wide kernel instantiated for one-triangle operand p.tri (1-4): through LDS, or streamed
 template <int FAM, bool GX>
 static hipError_t launch_wide_tri(const GemmProblem &p, hipStream_t s) {
-    if (RBH_STREAM_TRI && RBH_STREAM64 && !p.materialise) {
+    if (RBH_TRI_STREAMED && !p.materialise) {
         switch (p.tri) {
         case 1: return launch_stream<double, GEN_OK, FAM, GX, 1>(p, s);
         case 2: return launch_stream<double, GEN_OK, FAM, GX, 2>(p, s);
@@ -2048,7 +2004,7 @@ static GemmPlan plan_gemm(const GemmProblem &p) {
         return pl;
     }
     if (p.tri) {
-        pl.kernel = RBH_STREAM_TRI && RBH_STREAM64 && !p.materialise ? PLAN_STREAM_TRI : PLAN_WIDE_TRI;   // as launch_wide_tri
+        pl.kernel = RBH_TRI_STREAMED && !p.materialise ? PLAN_STREAM_TRI : PLAN_WIDE_TRI;   // as launch_wide_tri
         pl.tiles = wide_tiles();
         pl.splitk = stream_geom<T>(p).split;   // as launch_wide
     } else if (stream_ok<T>(p)) {

@@ -1,0 +1,47 @@
+// variants.hpp -- the compile-time tuning switches of the hot kernels, in one place.
+//
+// Each default below is the measured winner on MI355X (DESIGN.md section 4 has the A/B numbers). A
+// variant library is built with other values by tools/build_variant.sh <name> "-DNAME=value ..." into
+// randblas_amd/_var/<name>.so and timed with RBH_LIB_PATH pointing at it (tools/variants.sh); the
+// product library always uses these defaults. Settings measured as losing were removed from the
+// source, not kept as switches.
+#pragma once
+
+// ---- skge_dense.hip: the streamed GEMM (skge_stream_kernel) ---------------------------------
+// memory-operand prefetch depth, in part-blocks ahead of their use: f64 7 (C2 7.97-7.98 ms against
+// 7.99-8.02 with 3), f32 3 (C4 4.08-4.11 against 4.18-4.20 with 1), the one-triangle forms 7
+#ifndef RBH_PF64
+#define RBH_PF64 7
+#endif
+#ifndef RBH_PF32
+#define RBH_PF32 3
+#endif
+#ifndef RBH_PF_TRI
+#define RBH_PF_TRI 7
+#endif
+// one-triangle symmetric operands (sketch_symmetric_triangle, packed A): 1 = the streamed kernel,
+// 0 = skge_wide_kernel's LDS transpose of the mirrored tiles
+#ifndef RBH_TRI_STREAMED
+#define RBH_TRI_STREAMED 0
+#endif
+
+// ---- saso.hip: the LDS-DMA SASO apply (saso_dma_kernel) --------------------------------------
+// log2 of the chunk depth (contracted indices per panel): 7 (64-deep chunks: 0.70-0.84 ms on C3)
+#ifndef SD_KCS_DEF
+#define SD_KCS_DEF 7
+#endif
+// panel buffers in the LDS ring, and panels in flight ahead of the walked one
+#ifndef SD_NB_DEF
+#define SD_NB_DEF 2
+#endif
+#ifndef SD_PD_DEF
+#define SD_PD_DEF 1
+#endif
+// pad each panel column by 8 B instead of XOR-swizzling its 16-B slots (conflict-free b64 reads)
+#ifndef SD_PAD8_DEF
+#define SD_PAD8_DEF 1
+#endif
+// waves that issue the panel copies (4: C3 0.57 ms; 8 0.58, 2 0.81, 16 0.61)
+#ifndef SD_CW_DEF
+#define SD_CW_DEF 4
+#endif

@@ -5,8 +5,9 @@ RCCL, then the HIP unpack on the exchange stream). Modes (argv[1]):
   small  dense row shards (chunks 1 and 3) and SASO column shards (chunks 1 and 4), each bitwise
          against one direct call;
   c4     the 8-GPU run's per-rank dense problem (BASELINE configs[3]): d = 256 rows at ro_s = 1792 of
-         DenseDist(2048, 32768), A 32768^2 f32, chunks = 4 -- the f32 wide kernel on column chunks
-         of 8192 whose own tile count (64) would pick split-K 4; every chunk uses the whole rank
+         DenseDist(2048, 32768), A 32768^2 f32, chunks = 4 -- the streamed f32 kernel (64 x 1024
+         tiles; the whole rank problem has 128 of them and splits K 2) on column chunks of 8192,
+         whose own tile count (32) would pick a larger split; every chunk uses the whole rank
          problem's split instead (dense_rank_compute), so the result is bitwise the unchunked call's;
          three column slices against the oracle within E, and the row sums;
   ns     the north star's --split-d per-rank problem at N = 8: d = 256 at ro_s = 1792 of

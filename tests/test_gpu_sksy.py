@@ -270,3 +270,52 @@ def test_sketch_symmetric_not_bitwise_symmetric(cuda):
                              sym_check_tol=1e-6)
     got = host(B)
     assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))
+
+
+# --------------------------------------------------------------------------------------------
+# The overlapped default (round 5): the check runs on the library's side stream beside the sketch,
+# which goes to a workspace and is committed to B (B = W + beta B) only if the check passed. The
+# result must be sketch_general's on the same matrix, bit for bit, and a failing check must leave B
+# as it was (the reference throws before sketching).
+# --------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("side", ["L", "R"])
+@pytest.mark.parametrize("layout", ["C", "R"])
+@pytest.mark.parametrize("n,d,beta", [(300, 40, 0.0), (512, 64, -0.5), (2304, 128, 0.0), (4096, 32, 2.0)])
+def test_sketch_symmetric_overlapped_bitwise(cuda, side, layout, n, d, beta):
+    """(n, d) include a split-K shape (4096 x 32: few output tiles) and a streamed-kernel shape."""
+    M = sym_full(n, 5)
+    A = dev(M.ravel(order="F" if layout == "C" else "C"), cuda)
+    S = rb.DenseSkOp(rb.DenseDist(d, n) if side == "L" else rb.DenseDist(n, d), rb.RNGState(3))
+    rows, cols = (d, n) if side == "L" else (n, d)
+    ldb = rows if layout == "C" else cols
+    B0 = O.random_matrix(rows, cols, 42)
+    got, exp = dev(B0, cuda), dev(B0, cuda)
+    if side == "L":
+        rb.sketch_symmetric_left(layout, d, n, 0.75, S, A, n, beta, got, ldb)
+        rb.sketch_general_left(layout, "N", "N", d, n, n, 0.75, S, A, n, beta, exp, ldb)
+    else:
+        rb.sketch_symmetric_right(layout, n, d, 0.75, A, n, S, beta, got, ldb)
+        rb.sketch_general_right(layout, "N", "N", n, d, n, 0.75, A, n, S, beta, exp, ldb)
+    assert rb.sketch_symmetric_last_path() == "full"
+    assert np.array_equal(host(got).view(np.uint64), host(exp).view(np.uint64))
+
+
+@pytest.mark.parametrize("where", ["device", "host"])
+def test_sketch_symmetric_failed_check_leaves_b(cuda, where):
+    """An A that fails the check: the call raises and B keeps its contents (device and host B)."""
+    n, d = 700, 48
+    M = sym_full(n, 6)
+    M[3, 650] += 1e-6
+    Af = M.ravel(order="F")
+    S = rb.DenseSkOp(rb.DenseDist(d, n), rb.RNGState(3))
+    B0 = O.random_matrix(d, n, 42)
+    B = dev(B0, cuda) if where == "device" else B0.copy()
+    A = dev(Af, cuda) if where == "device" else Af.copy()
+    with pytest.raises(rb.RandBLASError):
+        rb.sketch_symmetric_left("C", d, n, 1.0, S, A, n, 0.0, B, d)
+    got = host(B) if where == "device" else B
+    assert np.array_equal(got, B0)
+    # within tolerance: the sketch is committed
+    rb.sketch_symmetric_left("C", d, n, 1.0, S, A, n, 0.0, B, d, sym_check_tol=1e-3)
+    got = host(B) if where == "device" else B
+    assert not np.array_equal(got, B0)

@@ -129,8 +129,8 @@ def test_north_star_slices(cuda):
 @pytest.mark.parametrize("rank", [0, 7])
 def test_c4_per_gpu_shard(cuda, rank):
     """configs[3]: f32, d=2048 row-sharded over 8 GPUs -> d=256 rows per GPU at ro_s = 256 g of
-    DenseDist(2048, 32768), A 32768^2 f32 (4 GiB): the 64 x 512 f32 tile at full K. Slices at the
-    start, middle and end + row sums over all 32768 columns."""
+    DenseDist(2048, 32768), A 32768^2 f32 (4 GiB): the streamed f32 kernel's 64 x 1024 tiles with
+    split-K 2 at full K. Slices at the start, middle and end + row sums over all 32768 columns."""
     D, d, m, n = 2048, 256, 32768, 32768
     ro = rank * d
     A = device_A(cuda, m, n, torch.float32)
