@@ -77,13 +77,16 @@ __global__ __launch_bounds__(256) void symcheck_kernel(int64_t n, const T *A, in
 
 // The same check with few registers, for running beside the sketch GEMM (sketch_symmetric's
 // overlapped form): the streamed f64 GEMM keeps 240 of a SIMD lane's 512 registers for each of its two
-// waves, so a check wave fits beside them only with at most 32. Each thread moves four rows of a tile
-// at a time (four loads in flight instead of sixteen); the predicate, tiles and flags are the
-// kernel's above.
+// waves, so a check wave fits beside them only with at most 32. Tiles of 32 x 32 (8.4 KiB of LDS: with
+// the 64 x 64 tiles above, the LDS limits a CU to four such workgroups, and the compiler then reserves
+// 97 registers a wave, since that occupancy leaves them free), each thread four rows of a tile, four
+// loads in flight; the predicate and flags are the kernel's above.
 template <typename T>
-__global__ __launch_bounds__(256) void symcheck_lean_kernel(int64_t n, const T *A, int64_t irs, int64_t ics, T tol, int *flag) {
-    __shared__ T mir[64][65];
-    const int64_t nt = (n + 63) / 64;
+__global__ __launch_bounds__(256) void symcheck_lean_kernel(int64_t n, const T *A, int64_t irs, int64_t ics, T tol,
+                                                            int *flag) {
+    constexpr int TS = 32, TY = 8, Q = TS / TY;
+    __shared__ T mir[TS][TS + 1];
+    const int64_t nt = (n + TS - 1) / TS;
     const int64_t b0 = blockIdx.x;
     const double tt = 2.0 * (double)nt + 1.0;
     int64_t bi = (int64_t)((tt - sqrt(tt * tt - 8.0 * (double)b0)) * 0.5);
@@ -91,64 +94,50 @@ __global__ __launch_bounds__(256) void symcheck_lean_kernel(int64_t n, const T *
     while (bi > 0 && rstart(bi) > b0) --bi;
     while (rstart(bi + 1) <= b0) ++bi;
     const int64_t bj = bi + (b0 - rstart(bi));
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;   // 64 x 4
-    // Thread (tx, ty) takes index tx along A's contiguous direction and ty + 4 q along the other (stride
-    // ld): element q of tile (ti, tj) sits at tile_base(ti, tj) + q * 4 ld, one 64-bit base per tile.
+    const int tx = threadIdx.x % TS, ty = threadIdx.x / TS;   // 32 x 8
+    // Thread (tx, ty) takes index tx along A's contiguous direction and ty + 8 q along the other (stride
+    // ld): element q of tile (ti, tj) sits at tile_base(ti, tj) + q * 8 ld, one 64-bit base per tile.
     const bool cm = irs == 1;
     const int64_t ld = cm ? ics : irs;
     auto tile_base = [&](int64_t ti, int64_t tj, int64_t &xs, int64_t &ys) -> const T * {
         const int64_t tc = cm ? ti : tj, ts = cm ? tj : ti;   // tile index along / across the contiguous direction
-        xs = tc * 64 + tx;
-        ys = ts * 64 + ty;
+        xs = tc * TS + tx;
+        ys = ts * TS + ty;
         return A + (xs < n && ys < n ? xs + ys * ld : 0);
     };
-    const int64_t step = 4 * ld;
-    int64_t mx, my;
-    const T *mb = tile_base(bj, bi, mx, my);   // mirror tile A(bj*64 + r, bi*64 + c)
-#pragma unroll 1
-    for (int q0 = 0; q0 < 16; q0 += 4) {   // stored transposed: mir[c][r] = A(bj*64 + r, bi*64 + c)
-        T mv[4];
+    const int64_t step = TY * ld;
+    int64_t mx, my, ax, ay;
+    const T *mb = tile_base(bj, bi, mx, my);   // mirror tile A(bj*TS + r, bi*TS + c)
+    const T *ab = tile_base(bi, bj, ax, ay);   // this tile A(bi*TS + r, bj*TS + c)
+    T mv[Q], av[Q];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const bool in = mx < n && my + 4 * (q0 + q) < n;
-            mv[q] = in ? mb[(q0 + q) * step] : (T)0;
-        }
+    for (int q = 0; q < Q; ++q) mv[q] = mx < n && my + TY * q < n ? mb[q * step] : (T)0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int rr = ty + 4 * (q0 + q);
-            if (cm) mir[rr][tx] = mv[q];
-            else mir[tx][rr] = mv[q];
-        }
+    for (int q = 0; q < Q; ++q) {   // stored transposed: mir[c][r] = A(bj*TS + r, bi*TS + c)
+        const int rr = ty + TY * q;
+        if (cm) mir[rr][tx] = mv[q];
+        else mir[tx][rr] = mv[q];
     }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) av[q] = ax < n && ay + TY * q < n ? ab[q * step] : (T)0;
     __syncthreads();
     bool bad = false, bitdiff = false;
-    int64_t ax, ay;
-    const T *ab = tile_base(bi, bj, ax, ay);   // this tile A(bi*64 + r, bj*64 + c)
-#pragma unroll 1
-    for (int q0 = 0; q0 < 16; q0 += 4) {
-        T av[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const bool in = ax < n && ay + 4 * (q0 + q) < n;
-            av[q] = in ? ab[(q0 + q) * step] : (T)0;
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int rr = ty + 4 * (q0 + q);
-            // (gi, gj) of the element; the pair is checked once, from the strict upper triangle
-            const int64_t gi = cm ? ax : ay + 4 * (q0 + q), gj = cm ? ay + 4 * (q0 + q) : ax;
-            const int lr = cm ? tx : rr, lc = cm ? rr : tx;
-            if (gi < n && gj < n && gi < gj) {
-                const T aij = av[q];
-                const T aji = mir[lr][lc];
-                const T dd = aij - aji;
-                const T viol = dd < (T)0 ? -dd : dd;
-                const T rel = ((aij < (T)0 ? -aij : aij) + (aji < (T)0 ? -aji : aji) + (T)1) * tol;
-                if (viol > rel) bad = true;
-                if (sizeof(T) == 8 ? __double_as_longlong((double)aij) != __double_as_longlong((double)aji)
-                                   : __float_as_uint((float)aij) != __float_as_uint((float)aji))
-                    bitdiff = true;
-            }
+    for (int q = 0; q < Q; ++q) {
+        const int rr = ty + TY * q;
+        // (gi, gj) of the element; the pair is checked once, from the strict upper triangle
+        const int64_t gi = cm ? ax : ay + TY * q, gj = cm ? ay + TY * q : ax;
+        const int lr = cm ? tx : rr, lc = cm ? rr : tx;
+        if (gi < n && gj < n && gi < gj) {
+            const T aij = av[q];
+            const T aji = mir[lr][lc];
+            const T dd = aij - aji;
+            const T viol = dd < (T)0 ? -dd : dd;
+            const T rel = ((aij < (T)0 ? -aij : aij) + (aji < (T)0 ? -aji : aji) + (T)1) * tol;
+            if (viol > rel) bad = true;
+            if (sizeof(T) == 8 ? __double_as_longlong((double)aij) != __double_as_longlong((double)aji)
+                               : __float_as_uint((float)aij) != __float_as_uint((float)aji))
+                bitdiff = true;
         }
     }
     const int f = (__any(bad) ? 1 : 0) | (__any(bitdiff) ? 2 : 0);
@@ -172,7 +161,7 @@ __global__ void sksy_commit_kernel(int64_t M, int64_t N, const T *W, T beta, T *
 template <typename T>
 static hipError_t launch_sym_lean(char layout, const T *A, int64_t n, int64_t lda, T tol, int *flag, hipStream_t s) {
     if (n <= 1) return hipSuccess;
-    const int64_t nt = (n + 63) / 64;
+    const int64_t nt = (n + 31) / 32;
     const int64_t pairs = nt * (nt + 1) / 2;
     const int64_t irs = layout == 'C' ? 1 : lda, ics = layout == 'C' ? lda : 1;
     hipLaunchKernelGGL(symcheck_lean_kernel<T>, dim3((unsigned)pairs), dim3(256), 0, s, n, A, irs, ics, tol, flag);
