@@ -296,7 +296,8 @@ def run_config(args, config, prefilled, world, rank, dev, use_dist, cpu_target_s
         from randblas_amd.distributed import ColumnShardedSketch
 
         B_full = torch.empty(d * world * n, dtype=tdt, device=dev)
-        drv = ColumnShardedSketch(d, n, lambda j0, j1, out: compute(0, j0, j1, out), tdt, dev, chunks=args.chunks)
+        drv = ColumnShardedSketch(d, n, lambda j0, j1, out: compute(0, j0, j1, out), tdt, dev,
+                                  chunks=max(args.chunks, 1))
     elif use_dist:
         from randblas_amd.distributed import RowShardedSketch
 
@@ -307,7 +308,14 @@ def run_config(args, config, prefilled, world, rank, dev, use_dist, cpu_target_s
         else:
             from randblas_amd.distributed import dense_rank_compute
 
-            drv = RowShardedSketch(d_total, n, dense_rank_compute(S, A, lda, m, d, n), tdt, dev, chunks=args.chunks)
+            from randblas_amd.distributed import wave_chunks
+
+            chunks = args.chunks
+            if chunks == 0:   # auto: whole grid waves per chunk when ranks exchange (world > 1), else 1
+                pl = rb.plan_left("C", "N", "N", d, n, m, S, A, lda, d, ro_s=rank * d, dtype=dtype)
+                cus = torch.cuda.get_device_properties(dev).multi_processor_count
+                chunks = wave_chunks(pl.workgroups, cus, n, 1024) if world > 1 else 1
+            drv = RowShardedSketch(d_total, n, dense_rank_compute(S, A, lda, m, d, n), tdt, dev, chunks=chunks)
 
     if drv is not None:
         def step():
@@ -426,7 +434,8 @@ def run_config(args, config, prefilled, world, rank, dev, use_dist, cpu_target_s
                    "symmetry_check": ("tol=0, timed in the step" if kind == "sksy" else None),
                    "A_storage": {"sksy": "full", "sksyp": "packed upper (n(n+1)/2)"}.get(kind, "full"),
                    "parallelism": (f"{'column' if kind == 'saso' else 'row'}-shard x{world} + RCCL all-gather"
-                                   if use_dist else "single GPU")},
+                                   if use_dist else "single GPU"),
+                   "chunks": len(drv.cols) if drv is not None else None},
         "pct_of_peak": roof["frac"] * 100.0,
         # what kernel_ms and the roofline time; any other launch of the step is in ms_per_step only
         "dominant_kernel": {"dense": f"{kname} (one per chunk)",
@@ -451,9 +460,11 @@ def main():
                          "as sub-records of the same line)")
     ap.add_argument("--no-configs", action="store_true", help="the headline config only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--chunks", type=int, default=1,
+    ap.add_argument("--chunks", type=int, default=0,
                     help="column chunks per rank and step, each all-gathered as soon as it is done (N > 1 or --dist; "
-                         "every chunk uses the whole rank problem's split-K, so results do not depend on it)")
+                         "every chunk uses the whole rank problem's split-K, so results do not depend on it). "
+                         "0 = auto: dense ranks of a multi-GPU run cut their call into whole grid waves "
+                         "(distributed.wave_chunks), so a single call's gather overlaps its own compute; SASO 1")
     ap.add_argument("--dry-run", action="store_true", help="launch/report path only, no device work (CPU, gloo)")
     ap.add_argument("--lda-pad", type=int, default=0,
                     help="diagnostics: store the dense A with leading dimension m + pad (same matrix)")

@@ -71,6 +71,22 @@ def _unpack(src: torch.Tensor, nshards: int, rows: int, run: int, dst: torch.Ten
     view.copy_(src[:nshards * rows * run].view(nshards, rows, run))
 
 
+def wave_chunks(workgroups: int, cus: int, n: int, col_tile: int, most: int = 4) -> int:
+    """Column chunks for ONE sharded call whose exchange should overlap its own compute: the number
+    of whole grid waves in the rank's launch (workgroups / CUs) when the launch is exactly that many
+    full waves, at most `most`, and every chunk boundary lands on a tile boundary (n / chunks a
+    multiple of col_tile). Chunk c is then a full-chip launch, so cutting the call costs no occupancy,
+    and chunk c's all-gather runs under chunk c + 1's compute: a single call leaves only the last
+    chunk's gather exposed. 1 when the launch is one wave or less (nothing to overlap it with).
+    C2 weak at N = 8: d_loc 1024, n 16384 -> 512 tiles of 64 x 512 on 256 CUs -> 2 chunks of 8192."""
+    if cus <= 0 or workgroups < 2 * cus or workgroups % cus:
+        return 1
+    k = min(workgroups // cus, most)
+    while k > 1 and (workgroups % (k * cus) or n % k or (n // k) % col_tile):
+        k -= 1
+    return k
+
+
 def _column_chunks(n: int, chunks: int) -> List[Tuple[int, int]]:
     chunks = max(1, min(chunks, n))
     bounds = [round(i * n / chunks) for i in range(chunks + 1)]

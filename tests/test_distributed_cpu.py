@@ -139,3 +139,17 @@ def test_column_sharded_saso_gloo_world2(chunks):
     O.left_spmm_coo("C", "N", "N", d, n, m, 1.0, d, m, rows, cols, vals, 0, 0, A, m, 0.0, exp, d)
     for r in range(world):
         assert np.array_equal(results[r], exp)
+
+
+def test_wave_chunks_policy():
+    """A single sharded call is cut only into whole grid waves whose boundaries are tile boundaries."""
+    from randblas_amd.distributed import wave_chunks
+
+    assert wave_chunks(512, 256, 16384, 1024) == 2      # C2 weak at N = 8: two full-chip launches
+    assert wave_chunks(1024, 256, 16384, 1024) == 4     # NS weak at N = 8
+    assert wave_chunks(2048, 256, 16384, 1024) == 4     # capped
+    assert wave_chunks(256, 256, 32768, 1024) == 1      # one wave: nothing to overlap
+    assert wave_chunks(384, 256, 16384, 1024) == 1      # a partial wave: chunks would idle CUs
+    assert wave_chunks(768, 256, 3072, 1024) == 3
+    assert wave_chunks(768, 256, 2048, 1024) == 1       # 3 does not divide n; 2 does not divide the grid
+    assert wave_chunks(512, 0, 16384, 1024) == 1
