@@ -441,7 +441,7 @@ def run_config(args, config, prefilled, world, rank, dev, use_dist, cpu_target_s
         "dominant_kernel": {"dense": f"{kname} (one per chunk)",
                             "saso": "saso_dma_kernel (sampling and the CSR build: ms_per_step only)",
                             "sksy": f"{kname} (the symmetry check, the step's other launch: ms_per_step only)",
-                            "sksyp": "skge_wide_kernel<TRI 3>"}[kind],
+                            "sksyp": "skge_stream_kernel<TRI 3> (one-triangle, packed; + tri_diag_kernel)"}[kind],
         # the library's plan of the dense rank problem (rbh_lskge3_plan): kernel, split-K, tiles
         "plan": plan,
         "roofline": roof,

@@ -187,6 +187,7 @@ hipError_t ws_release(hipStream_t s, bool all) {
     }
     return hipSuccess;
 }
+
 }  // namespace rbh
 
 namespace {

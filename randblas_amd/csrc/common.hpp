@@ -54,6 +54,9 @@ struct GemmProblem {
     // or k >= o (2 full, 4 packed ptr[(k - o) + o*tri_n - o(o-1)/2]); the rest is its mirror (k, o).
     int tri;
     int64_t tri_n;
+    // the streamed one-triangle kernel's diagonal blocks, both triangles (tri_diag_kernel): block b
+    // (rows and columns 16 b .. 16 b + 15) at tri_diag[256 b], row-major
+    const void *tri_diag;
     // The generated operand materialised by the launcher (wide kernels, launch_gemm): element (o, k)
     // at gmat[o * K + k]; null = drawn inside the kernel.
     const void *gmat;
@@ -113,6 +116,7 @@ void timing_end(hipStream_t s);
 // Stream-ordered workspaces (capi.cpp): one arena of hipMalloc blocks per (device, stream), private
 // to this library; ws_release frees the idle blocks (rbh_release_workspaces).
 hipError_t ws_alloc(void **p, size_t bytes, hipStream_t s);
+
 hipError_t ws_free(void *p, hipStream_t s);
 hipError_t ws_release(hipStream_t s, bool all);
 

@@ -1209,6 +1209,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     constexpr int NH = NPART * FB;                        // part-blocks of a step (part FB + c)
     constexpr int NSLOT = PF + 1;                         // register slots of the memory prefetch ring
     static_assert(NH % NSLOT == 0, "a part-block's slot must not depend on the step");
+    static_assert(TRI == 0 || (NPART == 2 && sizeof(T) == 8), "one-triangle operands: f64 64-row tiles (lane pairs)");
     // consumption order of a step's part-blocks: part-major (part p of every block, then part p + 1)
     // or block-major (CMAJOR: both parts of block c, then block c + 1); every accumulator sees the same
     // k order either way (its block's parts in turn), so the sums are the same bits
@@ -1225,6 +1226,8 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     typedef float pf_t __attribute__((ext_vector_type(4 * NLD)));
 
     __shared__ __attribute__((aligned(16))) char gring[2 * R * SLOT_B];
+    // one-triangle operand: each wave's mirrored part-blocks, NSLOT slots of 1 KiB (below)
+    __shared__ __attribute__((aligned(16))) char mring[TRI ? 8 * NSLOT * 1024 : 16];
     __shared__ rb::LogfEntry tab[16];
 
     const int tid = threadIdx.x;
@@ -1258,11 +1261,11 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     const uint64_t mbase = (uint64_t)(uintptr_t)(mptr + wbase * mop.so);
     uint32_t mb_lo = __builtin_amdgcn_readfirstlane((uint32_t)mbase), mb_hi = __builtin_amdgcn_readfirstlane((uint32_t)(mbase >> 32));
     asm volatile("" : "+s"(mb_lo), "+s"(mb_hi));
-    const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(uintptr_t)(((uint64_t)mb_hi << 32) | mb_lo), (short)0, -1, 0x00020000);
     // One-triangle operand (TRI 1-4, as skge_wide_kernel): element (o, k) is stored at rowbase(o) + k
     // inside the triangle and is the stored (k, o) outside; the resource is based at the matrix and
-    // the launcher checks that every byte offset of the stored triangle fits in 32 bits.
+    // the launcher checks that every byte offset of the stored triangle fits in 32 bits. Its range is
+    // the stored triangle (loads past it return 0): a mirrored pair load (below) of a row past the
+    // operand's last one reads past its stored row, for an output that is discarded.
     constexpr bool TKLE = TRI == 1 || TRI == 3;
     const uint32_t tso = (uint32_t)mop.so, tn = (uint32_t)p.tri_n;
     auto rowbase = [&](uint32_t a) -> uint32_t {
@@ -1270,6 +1273,9 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
         if (TRI == 4) return a * tn - a * (a + 1) / 2;
         return a * tso;
     };
+    const int32_t mrange = TRI == 0 ? -1 : (int32_t)((TRI <= 2 ? (tn - 1) * tso + tn : tn * (tn + 1) / 2) * (uint32_t)sizeof(T));
+    const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(uintptr_t)(((uint64_t)mb_hi << 32) | mb_lo), (short)0, mrange, 0x00020000);
     uint32_t voff[FB];
 #pragma unroll
     for (int c = 0; c < FB; ++c) {
@@ -1278,59 +1284,143 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
         voff[c] = TRI ? (uint32_t)((rowbase((uint32_t)row) + VPL * g) * sizeof(T))
                       : (uint32_t)(((row - wbase) * mop.so + (int64_t)VPL * g) * (int64_t)sizeof(T));
     }
-    // Mirrored steps read the lane's element (o, K0 + a + j), a = VPL g, as the stored (s + a, o) with
-    // s = K0 + j: rowbase(s + a) + o = rowbase(s) [uniform, soffset] + a so + o (full storage),
-    // + s a + a (a + 1) / 2 + o (packed lower), or + a n - s a - a (a + 1) / 2 + o (packed upper):
-    // a per-lane constant vmir[c] plus at most one multiply-add by the uniform s.
-    const uint32_t a8 = (uint32_t)(VPL * g * sizeof(T));
-    uint32_t vmir[TRI ? FB : 1];
+    // Mirrored part-blocks (BG = 64: a part-block is the lane's 2 values k = 4 g + 2 p + {0, 1} of row
+    // o = 16 c + r, i.e. 8 stored rows K0 + 4 g' + 2 p + e' x the block's 16 positions, 1 KiB) go
+    // through the wave's LDS slot: one LDS-DMA along the stored rows (lane L takes stored row j = L >> 3,
+    // a = 4 (j >> 1) + 2 p + (j & 1), positions o0 + 16 c + 2 (L & 7) + {0, 1}, landing at 16 L: row j's
+    // 16 positions at 128 j), then the lane's two values as ds_read_b64 at 256 g + 8 r and + 128 (each
+    // 16-lane group reads 128 contiguous bytes: no bank conflict). No VALU: a register pair swap here
+    // (lane-pair 16-B loads + DPP) took 8 VALU per part-block, and MFMAs hold their SIMD's VALU issue
+    // (C5p 4.52-4.54 ms). The values are moved, not computed: the MFMA sums are full storage's bits.
+    // Byte offset of lane L's copy: rowbase(K0 + a) + o = rowbase(K0) (uniform, soffset) + a lane
+    // constant (vdma[p]) + K0 a (packed lower) / - K0 a (packed upper) per step + 128 c (immediate).
+    uint32_t vdma[NPART], adma8[NPART];
     if (TRI) {
+        const uint32_t j = (uint32_t)lane >> 3, q = (uint32_t)lane & 7u;
 #pragma unroll
-        for (int c = 0; c < FB; ++c) {
-            int64_t row = wm0 + 16 * c + r;
-            row = row < mnO ? row : mnO - 1;
-            const uint32_t a = VPL * g, t0 = a * (a + 1) / 2;
-            const uint32_t lane_part = TRI <= 2 ? a * tso : (TRI == 3 ? t0 : a * tn - t0);
-            vmir[c] = (uint32_t)((lane_part + (uint32_t)row) * sizeof(T));
+        for (int pp = 0; pp < NPART; ++pp) {
+            const uint32_t a = 4u * (j >> 1) + (uint32_t)(PV * pp) + (j & 1u);
+            const uint32_t lane_part = TRI <= 2 ? a * tso : (TRI == 3 ? a * (a + 1) / 2 : a * tn - a * (a + 1) / 2);
+            vdma[pp] = (lane_part + (uint32_t)(wm0 < mnO ? wm0 : 0) + 2u * q) * (uint32_t)sizeof(T);
+            adma8[pp] = a * (uint32_t)sizeof(T);
         }
     }
-    // the step's class for this wave (uniform): 0 inside the triangle, 1 mirrored, 2 straddles the
-    // diagonal. The wave's rows (clamped) lie in [rlo, rhi].
-    const int rlo = (int)(wm0 < mnO ? wm0 : mnO - 1), rhi = (int)(wm0 + BMW - 1 < mnO ? wm0 + BMW - 1 : mnO - 1);
-    auto tclass = [&](int64_t kt) -> int {
-        const int K0 = (int)(kt * KS);
-        if (TKLE) return K0 + KS - 1 <= rlo ? 0 : (K0 > rhi ? 1 : 2);
-        return K0 >= rhi ? 0 : (K0 + KS - 1 < rlo ? 1 : 2);
+    const uint32_t mring0 = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)mring) + (uint32_t)wave * NSLOT * 1024u;
+    const uint32_t mrd = mring0 + (uint32_t)(256 * g + 8 * r);   // the lane's ds_read address in slot 0
+    const uint32_t mown = mring0 + 16u * (uint32_t)lane;          // its own 16 B of a lane-linear copy
+    // A part-block's two values out of its LDS slot, once its copy has landed (at most PF - 1 copies
+    // issued after it in flight: this read is issued one part-block ahead of its use): two 8-B reads,
+    // down the stored rows (mirrored: 256 g + 8 r, + 128) or the lane's own 16 B (inside / diagonal:
+    // 16 L, + 8). The reads are left in flight; the consumer waits (lgkmcnt) before its MFMAs.
+    T yb[2][2];
+    auto lds_read = [&](T (&y)[2], int slot, bool mir) {
+        if constexpr (TRI != 0) {
+            const uint32_t a0 = mir ? mrd : mown, a1 = mir ? mrd + 128u : mown + 8u;
+            asm volatile("s_waitcnt vmcnt(%2)\n\t"
+                         "ds_read_b64 %0, %3 offset:%5\n\t"
+                         "ds_read_b64 %1, %4 offset:%5"
+                         : "=&v"(y[0]), "=&v"(y[1])
+                         : "n"(PF - 1), "v"(a0), "v"(a1), "n"(slot * 1024)
+                         : "memory");
+        }
     };
+    typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+    u32x4_t mrs4 = {mb_lo, mb_hi & 0xffffu, (uint32_t)mrange, 0x00020000u};   // mrsrc as SGPRs for the asm copies
+    // Diagonal blocks (one-triangle operand): the 16 x 16 blocks on A's diagonal, expanded to both
+    // triangles in a small workspace before the launch (tri_diag_kernel; 2 KiB per block, row o's 16
+    // values contiguous), loaded like a block inside the triangle: lane (g, r) part p at 128 r + 32 g +
+    // 16 p of block K0 / 16. So every part-block of every step is one 16-B load.
+    uint32_t dm_lo = 0, dm_hi = 0;
+    if (TRI) {
+        const uint64_t dbase = (uint64_t)(uintptr_t)p.tri_diag;
+        dm_lo = __builtin_amdgcn_readfirstlane((uint32_t)dbase);
+        dm_hi = __builtin_amdgcn_readfirstlane((uint32_t)(dbase >> 32));
+        asm volatile("" : "+s"(dm_lo), "+s"(dm_hi));
+    }
+    const __amdgpu_buffer_rsrc_t drsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(uintptr_t)(((uint64_t)dm_hi << 32) | dm_lo), (short)0, (int32_t)(TRI ? tn * 16u * (uint32_t)sizeof(T) : 0u), 0x00020000);
+    const uint32_t vdiag = (uint32_t)(r * 16 * (int)sizeof(T) + VPL * g * (int)sizeof(T));
+    const u32x4_t drs4 = {dm_lo, dm_hi & 0xffffu, TRI ? tn * 16u * (uint32_t)sizeof(T) : 0u, 0x00020000u};
+    // The class of part-block (step kt, block c) for this wave (uniform; K0 and the block's first row
+    // are multiples of 16): 0 inside the stored triangle, 1 mirrored, 2 the diagonal block.
+    // Per step (uniform, formed once a step for the step the prefetches target): block c of step kt
+    // is the diagonal block if K0 = wm0 + 16 c (K0 and wm0 are multiples of 16), mirrored on the far
+    // side of it, inside the triangle on the near side; cd = (K0 - wm0) / 16. The offsets are split so
+    // that the part-block's constant 128 c + 16 p is the load's immediate for every class: the
+    // vector offset is one of three bases (two selects), the scalar offset one of three values.
+    struct TriStep {
+        int32_t cd;          // block index of the diagonal (may lie outside 0 .. FB - 1)
+        uint32_t so_mir;     // rowbase(K0) bytes
+        uint32_t so_dia;     // K0 * 128: block K0 / 16 of the diagonal workspace
+        uint32_t so_in;      // kt * 128
+        uint32_t md[NPART];  // mirrored copy offset of part p: vdma[p] +- K0 a
+    };
+    const int32_t wm0_32 = (int32_t)wm0;   // (32-bit: the SALU compares; operands < 2^31 rows)
+    auto tri_step = [&](int64_t kt) -> TriStep {
+        TriStep t{};
+        if constexpr (TRI != 0) {
+            const uint32_t K0 = (uint32_t)kt * KS;
+            t.cd = ((int32_t)K0 - wm0_32) >> 4;
+            t.so_mir = rowbase(K0) * (uint32_t)sizeof(T);
+            t.so_dia = K0 * 16u * (uint32_t)sizeof(T);
+            t.so_in = (uint32_t)kt * 128u;
+#pragma unroll
+            for (int pp = 0; pp < NPART; ++pp) {
+                uint32_t m = vdma[pp];
+                if (TRI == 3) m += __umul24(K0, adma8[pp]);
+                if (TRI == 4) m -= __umul24(K0, adma8[pp]);
+                t.md[pp] = m;
+            }
+        }
+        return t;
+    };
+    auto is_mir = [&](const TriStep &t, int c) -> bool { return TKLE ? c < t.cd : c > t.cd; };
+    // in-triangle bases less their immediate 128 c (the immediate adds it back)
+    uint32_t voffi[TRI ? FB : 1];
+    if (TRI) {
+#pragma unroll
+        for (int c = 0; c < FB; ++c) voffi[c] = voff[c] - (uint32_t)(128 * c);
+    }
     // part p contracts the lane's values v = PV p .. PV p + PV - 1 (its 16-B slots 2 g + NLD p + l,
     // l < NLD); the ring holds part-blocks
     hv_t mv[NSLOT];
-    auto mload = [&](int slot, int i, int64_t kt) {   // part-block i = p FB + c of step kt
+    auto mload = [&](int slot, int i, int64_t kt, const TriStep &ts_) {   // part-block i = p FB + c of step kt
         const uint32_t soff = (uint32_t)(kt * 128);
         if constexpr (TRI != 0) {
-            const int cls = tclass(kt);
-            if (cls != 0) {   // mirrored or straddling: one 8-B load per element
-                const int c = i % FB;
-                const uint32_t K0 = (uint32_t)(kt * KS);
-#pragma unroll
-                for (int e = 0; e < PV; ++e) {
-                    const uint32_t j = (uint32_t)(PV * (i / FB) + e), sk = K0 + j;
-                    uint32_t vo = vmir[c];
-                    if (TRI == 3) vo += sk * a8;
-                    if (TRI == 4) vo -= sk * a8;
-                    uint32_t so_ = rowbase(sk) * (uint32_t)sizeof(T);
-                    if (cls == 2) {   // per element: inside (rowbase(o) + k) or mirrored
-                        int64_t row = wm0 + 16 * c + r;
-                        row = row < mnO ? row : mnO - 1;
-                        const uint32_t k = sk + VPL * g;
-                        const bool in = TKLE ? k <= (uint32_t)row : k >= (uint32_t)row;
-                        vo = in ? voff[c] + sk * (uint32_t)sizeof(T) : vo + so_;
-                        so_ = 0;
-                    }
-                    mv[slot][e] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(mrsrc, vo, so_, 0));
-                }
-                return;
+            // one 16-B load whatever the class, its resource and offsets picked by selects on the
+            // uniform class: control flow here (the per-element straddle loads of round 4) left the
+            // compiler unable to count the prefetch ring's loads, and it waited for each one at once
+            // (vmcnt(0)/(1) where the plain kernel waits with vmcnt(7))
+            // every class through the wave's LDS slot by LDS-DMA (asm: the compiler sees no VMEM
+            // in this loop, so nothing of its own waits on these copies; the consumer counts them).
+            // Constant offsets ride in soffset: an LDS-DMA's immediate offset moves its LDS
+            // destination as well as its source.
+            const int c = i % FB, pp = i / FB;
+            const uint32_t m0v = mring0 + (uint32_t)slot * 1024u;
+            if (is_mir(ts_, c)) {   // mirrored: along the stored rows (vdma), read back transposed
+                asm volatile("s_mov_b32 m0, %0\n\t"
+                             "s_nop 0\n\t"
+                             "buffer_load_dwordx4 %1, %2, %3 offen lds"
+                             :
+                             : "s"(m0v), "v"(ts_.md[pp]), "s"(mrs4), "s"(ts_.so_mir + (uint32_t)(16 * c * (int)sizeof(T)))
+                             : "memory", "m0");
+            } else if (c == ts_.cd) {   // the diagonal block, from the workspace
+                asm volatile("s_mov_b32 m0, %0\n\t"
+                             "s_nop 0\n\t"
+                             "buffer_load_dwordx4 %1, %2, %3 offen lds"
+                             :
+                             : "s"(m0v), "v"(vdiag), "s"(drs4), "s"(ts_.so_dia + (uint32_t)(16 * pp))
+                             : "memory", "m0");
+            } else {   // inside the triangle: the lane's own 16 B, as full storage
+                asm volatile("s_mov_b32 m0, %0\n\t"
+                             "s_nop 0\n\t"
+                             "buffer_load_dwordx4 %1, %2, %3 offen lds"
+                             :
+                             : "s"(m0v), "v"(voff[c]), "s"(mrs4), "s"(ts_.so_in + (uint32_t)(16 * pp))
+                             : "memory", "m0");
             }
+            return;
         }
         pf_t x;
 #pragma unroll
@@ -1429,8 +1519,10 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
 #pragma unroll
     for (int u = 0; u < WCALLS; ++u) draw(u, kt0, 0, kt1);
     if (kt0 < kt1) {
+        const TriStep t0 = tri_step(kt0);
 #pragma unroll
-        for (int i = 0; i < PF; ++i) mload(i % NSLOT, CMAJOR ? seq_block(i) : i, kt0);
+        for (int i = 0; i < PF; ++i) mload(i % NSLOT, CMAJOR ? seq_block(i) : i, kt0, t0);
+        if constexpr (TRI != 0) lds_read(yb[0], 0, is_mir(t0, 0));   // the first part-block's values
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
@@ -1442,6 +1534,9 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
         for (int ts = 0; ts < R; ++ts) {
             const int64_t kt = kr0 + ts;
             if (kt >= kt1) break;
+            // one-triangle operand: this step's and the next one's classes and offsets (the next
+            // step's part-blocks are the ones the prefetches of this step load)
+            const TriStep tsc = tri_step(kt), tsn = tri_step(kt + 1 < kt1 ? kt + 1 : kt);
             if (CMAJOR) {
                 // block-major: both parts of block c back to back, so the two 16-B halves a lane
                 // takes of its row's 128-B line are requested PF part-blocks apart, not half a step
@@ -1456,7 +1551,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
                     for (int h = 0; h < NPART; ++h) {
                         const int s = c * NPART + h, sn = s + PF;
                         const int64_t ktn = sn < NH ? kt : (kt + 1 < kt1 ? kt + 1 : kt);
-                        mload(sn % NSLOT, seq_block(sn % NH), ktn);
+                        mload(sn % NSLOT, seq_block(sn % NH), ktn, tsn);
                         // keep the load here, PF part-blocks ahead of its use (the scheduler otherwise
                         // sinks it next to its MFMAs and waits on it at once)
                         __builtin_amdgcn_sched_barrier(0);
@@ -1479,9 +1574,35 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
                     // part-block i + PF (this step's, or the next step's first ones), PF ahead
                     const int i = h * FB + c, in = i + PF;
                     const int64_t ktn = in < NH ? kt : (kt + 1 < kt1 ? kt + 1 : kt);
-                    mload(in % NSLOT, in % NH, ktn);
+                    mload(in % NSLOT, in % NH, ktn, in < NH ? tsc : tsn);
                     __builtin_amdgcn_sched_barrier(0);   // (as above)
-                    const hv_t &m = mv[i % NSLOT];
+                    hv_t m;
+                    if constexpr (TRI == 0) {
+                        m = mv[i % NSLOT];
+                    } else {
+                        // this part-block's values were read from LDS during the previous part-block
+                        // (yb[i & 1]); the read of the next one starts now, under this one's MFMAs
+                        T (&cur)[2] = yb[i & 1];
+                        if (c == 0) {
+                            // first part-block of a part: the generated fragments (gf, read just above)
+                            // complete with it, inside this wait, so the compiler puts no wait of its own
+                            // before the MFMAs -- its count cannot see the read issued below and would
+                            // wait for that too
+                            static_assert(FA == 4, "four generated fragments per part");
+                            asm volatile("s_waitcnt lgkmcnt(0)"
+                                         : "+v"(cur[0]), "+v"(cur[1]), "+v"(gf[0]), "+v"(gf[1]), "+v"(gf[2]), "+v"(gf[3])
+                                         :
+                                         : "memory");
+                        } else {
+                            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur[0]), "+v"(cur[1]) : : "memory");
+                        }
+                        if (i + 1 < NH) lds_read(yb[(i + 1) & 1], (i + 1) % NSLOT, is_mir(tsc, (i + 1) % FB));
+                        else lds_read(yb[(i + 1) & 1], (i + 1) % NSLOT, is_mir(tsn, 0));
+                        // (the read stays ahead of this part-block's MFMAs, in its own registers)
+                        __builtin_amdgcn_sched_barrier(0);
+                        m[0] = cur[0];
+                        m[1] = cur[1];
+                    }
 #pragma unroll
                     for (int e = 0; e < PV; ++e)
 #pragma unroll
@@ -1500,6 +1621,10 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
+
+    // the one-triangle copies the compiler cannot see: the last (clamped) ones land before the
+    // workgroup's LDS can be handed to another
+    if constexpr (TRI != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     // split-K: alpha times this split's partial sum to partial[z]; the reduction adds them in order
     T *C = SPLIT ? (T *)p.partial + z * p.M * p.N : (T *)p.C;
@@ -1878,6 +2003,20 @@ static bool stream_ok(const GemmProblem &p) {
     return !p.materialise && (sizeof(T) == 8 ? wide_ok<T>(p) : wide32_ok<T>(p));
 }
 
+// The diagonal 16 x 16 blocks of a one-triangle symmetric operand (TRI 1-4, GemmProblem::tri) in
+// both triangles, for skge_stream_kernel's diagonal part-blocks: block b at D[256 b], row-major.
+// Element (o, k) is the stored (o, k) on the stored side of the diagonal, else the stored (k, o).
+template <int TRI>
+__global__ __launch_bounds__(256) void tri_diag_kernel(const double *A, int64_t so, int64_t n, double *D) {
+    const int64_t b = blockIdx.x;
+    const int o = threadIdx.x >> 4, k = threadIdx.x & 15;
+    const int64_t row = 16 * b + o, col = 16 * b + k;
+    const bool stored = (TRI == 1 || TRI == 3) ? col <= row : col >= row;
+    const int64_t sr = stored ? row : col, sc = stored ? col : row;
+    const int64_t base = TRI == 3 ? sr * (sr + 1) / 2 : (TRI == 4 ? sr * n - sr * (sr + 1) / 2 : sr * so);
+    D[256 * b + threadIdx.x] = A[base + sc];
+}
+
 // part-blocks loaded ahead of their use (a register ring of PF + 1; PF + 1 divides 8)
 template <typename T> constexpr int stream_pf() { return sizeof(T) == 8 ? RBH_PF64 : RBH_PF32; }
 
@@ -1895,6 +2034,21 @@ static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
     if (split > 1) {
         e = ws_alloc(&q.partial, sizeof(T) * (size_t)split * p.M * p.N, s);
         if (e != hipSuccess) return e;
+    }
+    void *diag = nullptr;
+    if constexpr (TRI != 0) {   // the operand's diagonal blocks, both triangles (tri_diag_kernel)
+        const MemOperand &mo = GX ? p.ym : p.xm;
+        e = ws_alloc(&diag, sizeof(double) * 256 * (size_t)(p.tri_n / 16), s);
+        if (e == hipSuccess && p.tri_n >= 16)
+            hipLaunchKernelGGL(tri_diag_kernel<TRI>, dim3((unsigned)(p.tri_n / 16)), dim3(256), 0, s,
+                               (const double *)mo.ptr, mo.so, p.tri_n, (double *)diag);
+        if (e == hipSuccess) e = hipGetLastError();
+        if (e != hipSuccess) {
+            if (split > 1) (void)ws_free(q.partial, s);
+            if (diag) (void)ws_free(diag, s);
+            return e;
+        }
+        q.tri_diag = diag;
     }
     timing_begin(s);
     const dim3 grid((unsigned)(nb * split));
@@ -1922,13 +2076,18 @@ static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
         const hipError_t e2 = ws_free(q.partial, s);
         if (e == hipSuccess) e = e2;
     }
+    if (diag) {
+        const hipError_t e2 = ws_free(diag, s);
+        if (e == hipSuccess) e = e2;
+    }
     return e;
 }
 
-// The one-triangle operand stays on skge_wide_kernel by default: streamed, each mirrored step
-// loads 8 B per element (the stored row k holds the lane's row o at a 16-row stride), and C5p
-// measured 4.85 ms against 4.59-4.61 ms through the wide kernel's LDS transpose (same box, two
-// alternations; with PF 3 5.27-5.30 ms). RBH_TRI_STREAMED=1 builds stream it (variants.hpp).
+// The one-triangle operand streams by default (RBH_TRI_STREAMED, variants.hpp): skge_stream_kernel
+// with TRI, every part-block through the wave's LDS slot (mirrored ones transposed there), the
+// diagonal blocks from tri_diag_kernel's workspace. C5p (packed, d = 512, n = 16384): 4.31-4.32 ms
+// against 4.59-4.61 ms through the wide kernel's LDS transpose (round 4's streamed form with 8-B
+// loads per mirrored element: 4.85). The materialised-window option keeps the wide kernel.
 // the wide kernel instantiated for one-triangle operand p.tri (1-4): through LDS, or streamed
 template <int FAM, bool GX>
 static hipError_t launch_wide_tri(const GemmProblem &p, hipStream_t s) {

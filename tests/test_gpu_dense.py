@@ -429,3 +429,38 @@ def test_release_workspaces(cuda):
         del st
     rb.release_workspaces()
     assert np.array_equal(out[0].view(np.uint64), out[1].view(np.uint64))
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_split_repeat_and_graph_capture(cuda, dtype):
+    """Split-K on the streamed kernel (partials in a stream workspace, then the ordered reduction):
+    repeated calls, interleaved calls with a larger grid (the workspace grows), and a call captured
+    into a HIP graph and replayed all give the same bits."""
+    npdt = np.float64 if dtype == "f64" else np.float32
+    tdt = torch.float64 if dtype == "f64" else torch.float32
+    d, m, n = 64, 4096, 1100
+    A = dev(O.random_matrix(m, n, 7, npdt), cuda)
+    S = rb.DenseSkOp(rb.DenseDist(d, m), rb.RNGState(5))
+    assert rb.plan_left("C", "N", "N", d, n, m, S, A, m, d, dtype=dtype).splitk > 1
+    ref = torch.empty(d * n, dtype=tdt, device=cuda)
+    rb.sketch_general_left("C", "N", "N", d, n, m, 1.0, S, A, m, 0.0, ref, d)
+    exp = host(ref).copy()
+    big = dev(O.random_matrix(m, 8 * n, 8, npdt), cuda)   # more tiles: the counter block grows
+    Bb = torch.empty(d * 8 * n, dtype=tdt, device=cuda)
+    B = torch.empty_like(ref)
+    for _ in range(3):
+        rb.sketch_general_left("C", "N", "N", d, 8 * n, m, 1.0, S, big, m, 0.0, Bb, d)
+        B.fill_(float("nan"))
+        rb.sketch_general_left("C", "N", "N", d, n, m, 1.0, S, A, m, 0.0, B, d)
+        assert np.array_equal(host(B), exp)
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        rb.sketch_general_left("C", "N", "N", d, n, m, 1.0, S, A, m, 0.0, B, d)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        rb.sketch_general_left("C", "N", "N", d, n, m, 1.0, S, A, m, 0.0, B, d)
+    B.fill_(float("nan"))
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(host(B), exp)
