@@ -506,15 +506,28 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    head = run_config(args, headline, args.prefilled, world, rank, dev, use_dist, args.cpu_seconds)
+    # Every config's GPU timing first, back to back; the CPU baselines (seconds of host work during
+    # which the GPU idles and its clocks drop) after all of them. Timed right after a multi-second
+    # idle, a short config measures the clock ramp: C3 (0.6 ms steps, 13 with warm-up) read 0.606-
+    # 0.609 ms after an idle and 0.557-0.590 ms after GPU work (profiles/r05/c3_order_effect.txt).
+    head = run_config(args, headline, args.prefilled, world, rank, dev, use_dist, 0)
     sub = {}
     for name, cfg, pre in subs:
         try:
-            sub[name] = run_config(args, cfg, pre, world, rank, dev, use_dist, args.cpu_seconds / 3.0)
+            sub[name] = run_config(args, cfg, pre, world, rank, dev, use_dist, 0)
         except Exception as e:  # a failing sub-config never loses the headline line
             log(f"bench: config {name} failed: {e!r}")
             sub[name] = {"error": repr(e)}
             torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        for rec, cfg, target in [(head, headline, args.cpu_seconds)] + [
+                (sub[name], cfg, args.cpu_seconds / 3.0) for name, cfg, _ in subs if "error" not in sub[name]]:
+            kind, dtype, _, m, n, vec_nnz = CONFIGS[cfg]
+            try:   # this process's rows of the workload (d_per_gpu), as timed on the GPU
+                rec["cpu_baseline"] = cpu_baseline(kind, dtype, rec["config"]["d_per_gpu"], m, n, vec_nnz,
+                                                   target_s=target)
+            except Exception as e:  # the baseline never blocks the GPU line
+                log(f"cpu_baseline failed: {e!r}")
 
     if rank == 0:
         line = {"metric": "sketched-entries/sec (d*n/s) + achieved-%-of-fp64-MFMA-peak, skge d x m * m x n",
