@@ -237,10 +237,10 @@ SUB_CONFIGS = [("ns", "ns", False), ("c3", "c3", False), ("c3_prefilled", "c3", 
                ("c5", "c5", False), ("c5p", "c5p", False), ("c1", "c1", False)]
 
 
-def run_config(args, config, prefilled, world, rank, dev, use_dist, cpu_target_s):
+def run_config(args, config, prefilled, world, rank, dev, use_dist):
     """Time args.steps steps of one workload (after args.warmup untimed ones) and return its record:
-    step time (max over ranks), the dominant kernel's event time and roofline, the plan, and (rank 0,
-    one GPU) the CPU baseline. The device memory of the workload is released before returning."""
+    step time (max over ranks), the dominant kernel's event time and roofline and the plan (main()
+    adds the CPU baseline afterwards). The device memory of the workload is released before returning."""
     gc.collect()               # the previous workload's tensors (freed when its call returned)
     torch.cuda.empty_cache()
     kind, dtype, d, m, n, vec_nnz = CONFIGS[config]
@@ -402,13 +402,6 @@ def run_config(args, config, prefilled, world, rank, dev, use_dist, cpu_target_s
         plan = {"kernel": pl.kernel, "splitk": pl.splitk, "tiles": pl.tiles, "workgroups": pl.workgroups}
         kname = KERNEL_NAMES.get(pl.kernel, pl.kernel)
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and cpu_target_s > 0:
-        try:
-            cpu = cpu_baseline(kind, dtype, d, m, n, vec_nnz, target_s=cpu_target_s)
-        except Exception as e:  # the baseline never blocks the GPU line
-            log(f"cpu_baseline failed: {e!r}")
-
     return {
         # d x (world n) entries for SASO, d_total x n dense
         "value": (world * d * n if kind == "saso" else d_total * n) / (ms_step * 1e-3),
@@ -445,7 +438,7 @@ def run_config(args, config, prefilled, world, rank, dev, use_dist, cpu_target_s
         # the library's plan of the dense rank problem (rbh_lskge3_plan): kernel, split-K, tiles
         "plan": plan,
         "roofline": roof,
-        "cpu_baseline": cpu,
+        "cpu_baseline": None,
     }
 
 
@@ -510,11 +503,11 @@ def main():
     # which the GPU idles and its clocks drop) after all of them. Timed right after a multi-second
     # idle, a short config measures the clock ramp: C3 (0.6 ms steps, 13 with warm-up) read 0.606-
     # 0.609 ms after an idle and 0.557-0.590 ms after GPU work (profiles/r05/c3_order_effect.txt).
-    head = run_config(args, headline, args.prefilled, world, rank, dev, use_dist, 0)
+    head = run_config(args, headline, args.prefilled, world, rank, dev, use_dist)
     sub = {}
     for name, cfg, pre in subs:
         try:
-            sub[name] = run_config(args, cfg, pre, world, rank, dev, use_dist, 0)
+            sub[name] = run_config(args, cfg, pre, world, rank, dev, use_dist)
         except Exception as e:  # a failing sub-config never loses the headline line
             log(f"bench: config {name} failed: {e!r}")
             sub[name] = {"error": repr(e)}

@@ -5,7 +5,7 @@ import bench
 ap = argparse.Namespace(steps=10, warmup=3, chunks=0, lda_pad=0, split_d=False, no_cpu_baseline=True, prefilled=False, dist=False, gpus=1)
 dev = torch.device("cuda", 0)
 def run(cfg):
-    r = bench.run_config(ap, cfg, False, 1, 0, dev, False, 0)
+    r = bench.run_config(ap, cfg, False, 1, 0, dev, False)
     return round(r["kernel_ms"], 4), round(r["ms_per_step"], 4)
 print("c3 first", run("c3"), flush=True)
 print("c2", run("c2"), flush=True)
