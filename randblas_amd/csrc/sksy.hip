@@ -144,6 +144,114 @@ __global__ __launch_bounds__(256) void symcheck_lean_kernel(int64_t n, const T *
     if (f && (threadIdx.x & 63) == 0) atomicOr(flag, f);
 }
 
+// The check beside the GEMM, persistent and by LDS-DMA (f64): one workgroup of 4 waves per CU, each
+// wave walking its share of the 16 x 16 tile pairs (tile (bi, bj), bi <= bj, and its mirror (bj, bi))
+// with a ring of 4 pair slots (4 KiB each) copied 3 pairs ahead of the compare, so 12 KiB are in flight
+// per wave without holding them in registers. Beside the streamed GEMM (two waves of 240 registers
+// per SIMD, 64.5 KiB of LDS) it fits in 32 registers and 64 KiB. The non-persistent lean kernel above,
+// one workgroup per tile pair, finished 0.27 ms after the 4.03-ms GEMM at C5 (its workgroups only
+// ever held a few loads in flight beside it); the GEMM's own HBM use is 0.55 TB/s, so a check with
+// enough bytes in flight has the bandwidth to finish under it.
+// The matrix is read as column-major with leading dimension ld whatever its layout: the predicate
+// is symmetric in (A(i,j), A(j,i)), so a row-major A checks as its transpose. Copies are inline asm
+// (one LDS-DMA per 1 KiB, M0 = destination; an LDS-DMA's immediate offset would move the
+// destination too) and their waits are counted here: the compiler sees no VMEM in the loop.
+constexpr int SCD_SLOTS = 4;
+__global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(32))) void symcheck_dma_kernel(
+    int64_t n, const double *A, int64_t ld, double tol, uint32_t nbytes, int *flag) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    // the ring is dynamic LDS (4 * SLOTS * 4 KiB at launch): with a static 64 KiB the compiler sees an
+    // LDS-limited occupancy and gives the kernel 176 registers a wave "for free", which then no longer
+    // fit beside the GEMM (round 5, measured: the check ran after it)
+    extern __shared__ __attribute__((aligned(16))) char ring[];
+    // the check's few instructions before the GEMM's: without it the older GEMM waves take nearly every
+    // issue slot and the check ended 0.19 ms after the GEMM (C5, round 5)
+    __builtin_amdgcn_s_setprio(3);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t nt = (n + 15) / 16, pairs = nt * (nt + 1) / 2;
+    // this wave's pairs: a contiguous range of the row-by-row order of the upper block triangle
+    const int64_t gw = (int64_t)blockIdx.x * 4 + wave, nw = (int64_t)gridDim.x * 4;
+    const int64_t per = (pairs + nw - 1) / nw, p0 = gw * per < pairs ? gw * per : pairs;
+    const int64_t mine = (p0 + per < pairs ? p0 + per : pairs) - p0;
+    const uint64_t abase = (uint64_t)(uintptr_t)A;
+    const u32x4 rs = {(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)abase),
+                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(abase >> 32)) & 0xffffu, nbytes, 0x00020000u};
+    // copy lane L: column L / 8 (+ 8 for the second KiB), rows 2 (L % 8), + 1 of the tile
+    const uint32_t loff = (uint32_t)(((lane >> 3) * ld + 2 * (lane & 7)) * (int64_t)sizeof(double));
+    const uint32_t half_b = (uint32_t)(8 * ld * (int64_t)sizeof(double));
+    const uint32_t ring0 = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)ring) + (uint32_t)wave * SCD_SLOTS * 4096u;
+    // (bi, bj) of pair p0 (once), then both cursors step along the row: bj + 1, or the next row's diagonal
+    int64_t bi0 = 0, bj0 = 0;
+    if (mine > 0) {   // (p0 < pairs: past the last row the row starts fall again and the search would not end)
+        const double tt = 2.0 * (double)nt + 1.0;
+        bi0 = (int64_t)((tt - sqrt(tt * tt - 8.0 * (double)p0)) * 0.5);
+        auto rstart = [&](int64_t r) { return r * nt - r * (r - 1) / 2; };
+        while (bi0 > 0 && rstart(bi0) > p0) --bi0;
+        while (rstart(bi0 + 1) <= p0) ++bi0;
+        bj0 = bi0 + (p0 - rstart(bi0));
+        bi0 = __builtin_amdgcn_readfirstlane((int)bi0);
+        bj0 = __builtin_amdgcn_readfirstlane((int)bj0);
+    }
+    auto advance = [&](int64_t &bi, int64_t &bj) {
+        if (++bj == nt) { ++bi; bj = bi; }
+    };
+    auto dma = [&](uint32_t m0, uint32_t so) {
+        asm volatile("s_mov_b32 m0, %0\n\t"
+                     "s_nop 0\n\t"
+                     "buffer_load_dwordx4 %1, %2, %3 offen lds"
+                     :
+                     : "s"(m0), "v"(loff), "s"(rs), "s"(so)
+                     : "memory", "m0");
+    };
+    // pair k of this wave into slot k % SLOTS: four copies (past the wave's range: tile (0, 0) again,
+    // never compared, so every pair issues the same four and the counted waits hold)
+    int64_t ibi = bi0, ibj = bj0;
+    auto issue = [&](int64_t k) {
+        const bool live = k < mine;
+        const int64_t bi = live ? ibi : 0, bj = live ? ibj : 0;
+        if (live) advance(ibi, ibj);
+        const uint32_t t1 = (uint32_t)((16 * bi + 16 * bj * ld) * (int64_t)sizeof(double));
+        const uint32_t t2 = (uint32_t)((16 * bj + 16 * bi * ld) * (int64_t)sizeof(double));
+        const uint32_t m = ring0 + (uint32_t)(k % SCD_SLOTS) * 4096u;
+        dma(m, t1);
+        dma(m + 1024u, t1 + half_b);
+        dma(m + 2048u, t2);
+        dma(m + 3072u, t2 + half_b);
+    };
+    bool bad = false, bitdiff = false;
+    const int c = lane >> 2, r0 = 4 * (lane & 3);   // the lane: column c, rows r0 .. r0 + 3 of tile (bi, bj)
+    for (int64_t k = 0; k < SCD_SLOTS - 1; ++k) issue(k);
+    int64_t bi = bi0, bj = bj0;
+    for (int64_t k = 0; k < mine; ++k) {
+        issue(k + SCD_SLOTS - 1);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (SCD_SLOTS - 1)) : "memory");
+        const char *b = ring + (wave * SCD_SLOTS + (int)(k % SCD_SLOTS)) * 4096;
+        const int64_t j = 16 * bj + c;
+#pragma unroll 2   // (two rows at a time: the kernel must stay within 32 registers)
+        for (int q = 0; q < 4; ++q) {
+            const int r = r0 + q;
+            const int64_t i = 16 * bi + r;
+            const double aij = *reinterpret_cast<const double *>(b + c * 128 + r * 8);          // A(i, j)
+            const double aji = *reinterpret_cast<const double *>(b + 2048 + r * 128 + c * 8);   // A(j, i)
+            if (i < n && j < n && i < j) {
+                const double dd = aij - aji;
+                const double viol = dd < 0.0 ? -dd : dd;
+                const double rel = ((aij < 0.0 ? -aij : aij) + (aji < 0.0 ? -aji : aji) + 1.0) * tol;
+                if (viol > rel) bad = true;
+                if (__double_as_longlong(aij) != __double_as_longlong(aji)) bitdiff = true;
+            }
+        }
+        advance(bi, bj);
+        // (the slot is copied into again SLOTS - 1 pairs later, after these reads: the compiler waits
+        // for them before the compares above use the values)
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tail copies land before the LDS is released
+    const int f = (__any(bad) ? 1 : 0) | (__any(bitdiff) ? 2 : 0);
+    if (f && lane == 0) atomicOr(flag, f);
+}
+
 // Overlapped sketch_symmetric's last step (on the sketch's stream, after the check): unless the check
 // failed (flag bit 0), the canonical col-major M x N output C = W + beta C, W holding alpha S A (the
 // GEMM epilogue's v; beta == 0: C = W), so C gets the bits the GEMM would have written into it.
@@ -161,6 +269,19 @@ __global__ void sksy_commit_kernel(int64_t M, int64_t N, const T *W, T beta, T *
 template <typename T>
 static hipError_t launch_sym_lean(char layout, const T *A, int64_t n, int64_t lda, T tol, int *flag, hipStream_t s) {
     if (n <= 1) return hipSuccess;
+    // f64 whose stored range fits 32-bit byte offsets: the persistent LDS-DMA check, one workgroup per CU
+    const int64_t last = ((n - 1) * lda + n) * (int64_t)sizeof(T);
+    if (sizeof(T) == 8 && last < ((int64_t)1 << 32) - (int64_t)16 * lda * 8) {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
+            (void)hipGetLastError();
+            cus = 256;
+        }
+        hipLaunchKernelGGL(symcheck_dma_kernel, dim3((unsigned)cus), dim3(256), 4 * SCD_SLOTS * 4096, s, n, (const double *)A, lda,
+                           (double)tol, (uint32_t)last, flag);
+        return hipGetLastError();
+    }
     const int64_t nt = (n + 31) / 32;
     const int64_t pairs = nt * (nt + 1) / 2;
     const int64_t irs = layout == 'C' ? 1 : lda, ics = layout == 'C' ? lda : 1;

@@ -319,3 +319,40 @@ def test_sketch_symmetric_failed_check_leaves_b(cuda, where):
     rb.sketch_symmetric_left("C", d, n, 1.0, S, A, n, 0.0, B, d, sym_check_tol=1e-3)
     got = host(B) if where == "device" else B
     assert not np.array_equal(got, B0)
+
+
+@pytest.mark.parametrize("n,lda", [(33, 33), (700, 709), (1040, 1040)])
+@pytest.mark.parametrize("layout", ["C", "R"])
+def test_sketch_symmetric_check_positions(cuda, n, lda, layout):
+    """The overlapped check (f64: the persistent LDS-DMA kernel over 16 x 16 tile pairs) finds a
+    single asymmetric pair wherever it sits -- the first tile, a diagonal tile, the last (partial)
+    tile row and column, with lda > n -- and a symmetric A passes with sketch_general's bits."""
+    d = 24
+    M = sym_full(n, 11)
+    S = rb.DenseSkOp(rb.DenseDist(d, n), rb.RNGState(4))
+    B0 = O.random_matrix(d, n, 42)
+
+    def stored(Mx):
+        X = np.zeros((lda, n) if layout == "C" else (n, lda))
+        if layout == "C":
+            X[:n, :] = Mx
+            return X.ravel(order="F")
+        X[:, :n] = Mx
+        return X.ravel(order="C")
+
+    Bx = dev(B0, cuda)
+    exp = dev(B0, cuda)
+    A = dev(stored(M), cuda)
+    rb.sketch_symmetric_left(layout, d, n, 1.0, S, A, lda, 0.0, Bx, d if layout == "C" else n)
+    rb.sketch_general_left(layout, "N", "N", d, n, n, 1.0, S, A, lda, 0.0, exp, d if layout == "C" else n)
+    assert np.array_equal(host(Bx).view(np.uint64), host(exp).view(np.uint64))
+    for (i, j) in [(0, 1), (5, 9), (n - 2, n - 1), (1, n - 1), (17 % n, min(31, n - 1))]:
+        if i == j:
+            continue
+        Mp = M.copy()
+        Mp[i, j] += 2.0 ** -40 * (1.0 + abs(Mp[i, j]))   # one triangle only
+        B = dev(B0, cuda)
+        with pytest.raises(rb.RandBLASError):
+            rb.sketch_symmetric_left(layout, d, n, 1.0, S, dev(stored(Mp), cuda), lda, 0.0, B,
+                                     d if layout == "C" else n)
+        assert np.array_equal(host(B), B0), (i, j)
