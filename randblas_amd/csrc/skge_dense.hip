@@ -1226,8 +1226,6 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     typedef float pf_t __attribute__((ext_vector_type(4 * NLD)));
 
     __shared__ __attribute__((aligned(16))) char gring[2 * R * SLOT_B];
-    // one-triangle operand: each wave's mirrored part-blocks, NSLOT slots of 1 KiB (below)
-    __shared__ __attribute__((aligned(16))) char mring[TRI ? 8 * NSLOT * 1024 : 16];
     __shared__ rb::LogfEntry tab[16];
 
     const int tid = threadIdx.x;
@@ -1285,48 +1283,25 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
                       : (uint32_t)(((row - wbase) * mop.so + (int64_t)VPL * g) * (int64_t)sizeof(T));
     }
     // Mirrored part-blocks (BG = 64: a part-block is the lane's 2 values k = 4 g + 2 p + {0, 1} of row
-    // o = 16 c + r, i.e. 8 stored rows K0 + 4 g' + 2 p + e' x the block's 16 positions, 1 KiB) go
-    // through the wave's LDS slot: one LDS-DMA along the stored rows (lane L takes stored row j = L >> 3,
-    // a = 4 (j >> 1) + 2 p + (j & 1), positions o0 + 16 c + 2 (L & 7) + {0, 1}, landing at 16 L: row j's
-    // 16 positions at 128 j), then the lane's two values as ds_read_b64 at 256 g + 8 r and + 128 (each
-    // 16-lane group reads 128 contiguous bytes: no bank conflict). No VALU: a register pair swap here
-    // (lane-pair 16-B loads + DPP) took 8 VALU per part-block, and MFMAs hold their SIMD's VALU issue
-    // (C5p 4.52-4.54 ms). The values are moved, not computed: the MFMA sums are full storage's bits.
-    // Byte offset of lane L's copy: rowbase(K0 + a) + o = rowbase(K0) (uniform, soffset) + a lane
-    // constant (vdma[p]) + K0 a (packed lower) / - K0 a (packed upper) per step + 128 c (immediate).
-    uint32_t vdma[NPART], adma8[NPART];
-    if (TRI) {
-        const uint32_t j = (uint32_t)lane >> 3, q = (uint32_t)lane & 7u;
+    // o = 16 c + r): two 8-B loads per lane straight into the register ring, element e from stored row
+    // K0 + a, a = 4 g + 2 p + e, at the lane's own position o (the 16 lanes of a row group read 128
+    // contiguous bytes of a stored row). Every class issues two loads a part-block (inside the
+    // triangle and on the diagonal: the lane's two consecutive values), so the consumer's count of the
+    // loads in flight after a part-block's is exact. The values are moved, not computed: the MFMA sums
+    // are full storage's bits. Byte offset: rowbase(K0 + a) + o = rowbase(K0) (uniform, soffset) + a
+    // lane constant (vmr) + K0 a (packed lower) / - K0 a (packed upper) per step + 128 c (immediate).
+    uint32_t vmr[TRI ? NPART * 2 : 1], amr8[TRI ? NPART * 2 : 1];
+    if constexpr (TRI != 0) {
 #pragma unroll
-        for (int pp = 0; pp < NPART; ++pp) {
-            const uint32_t a = 4u * (j >> 1) + (uint32_t)(PV * pp) + (j & 1u);
+        for (int pe = 0; pe < NPART * 2; ++pe) {
+            const uint32_t a = (uint32_t)(VPL * g + PV * (pe >> 1) + (pe & 1));
             const uint32_t lane_part = TRI <= 2 ? a * tso : (TRI == 3 ? a * (a + 1) / 2 : a * tn - a * (a + 1) / 2);
-            vdma[pp] = (lane_part + (uint32_t)(wm0 < mnO ? wm0 : 0) + 2u * q) * (uint32_t)sizeof(T);
-            adma8[pp] = a * (uint32_t)sizeof(T);
+            vmr[pe] = (lane_part + (uint32_t)(wm0 < mnO ? wm0 : 0) + (uint32_t)r) * (uint32_t)sizeof(T);
+            amr8[pe] = a * (uint32_t)sizeof(T);
         }
     }
-    const uint32_t mring0 = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)mring) + (uint32_t)wave * NSLOT * 1024u;
-    const uint32_t mrd = mring0 + (uint32_t)(256 * g + 8 * r);   // the lane's ds_read address in slot 0
-    const uint32_t mown = mring0 + 16u * (uint32_t)lane;          // its own 16 B of a lane-linear copy
-    // A part-block's two values out of its LDS slot, once its copy has landed (at most PF - 1 copies
-    // issued after it in flight: this read is issued one part-block ahead of its use): two 8-B reads,
-    // down the stored rows (mirrored: 256 g + 8 r, + 128) or the lane's own 16 B (inside / diagonal:
-    // 16 L, + 8). The reads are left in flight; the consumer waits (lgkmcnt) before its MFMAs.
-    T yb[2][2];
-    auto lds_read = [&](T (&y)[2], int slot, bool mir) {
-        if constexpr (TRI != 0) {
-            const uint32_t a0 = mir ? mrd : mown, a1 = mir ? mrd + 128u : mown + 8u;
-            asm volatile("s_waitcnt vmcnt(%2)\n\t"
-                         "ds_read_b64 %0, %3 offset:%5\n\t"
-                         "ds_read_b64 %1, %4 offset:%5"
-                         : "=&v"(y[0]), "=&v"(y[1])
-                         : "n"(PF - 1), "v"(a0), "v"(a1), "n"(slot * 1024)
-                         : "memory");
-        }
-    };
     typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-    u32x4_t mrs4 = {mb_lo, mb_hi & 0xffffu, (uint32_t)mrange, 0x00020000u};   // mrsrc as SGPRs for the asm copies
+    u32x4_t mrs4 = {mb_lo, mb_hi & 0xffffu, (uint32_t)mrange, 0x00020000u};   // mrsrc as SGPRs for the asm loads
     // Diagonal blocks (one-triangle operand): the 16 x 16 blocks on A's diagonal, expanded to both
     // triangles in a small workspace before the launch (tri_diag_kernel; 2 KiB per block, row o's 16
     // values contiguous), loaded like a block inside the triangle: lane (g, r) part p at 128 r + 32 g +
@@ -1354,7 +1329,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
         uint32_t so_mir;     // rowbase(K0) bytes
         uint32_t so_dia;     // K0 * 128: block K0 / 16 of the diagonal workspace
         uint32_t so_in;      // kt * 128
-        uint32_t md[NPART];  // mirrored copy offset of part p: vdma[p] +- K0 a
+        uint32_t mr[NPART * 2];   // mirrored load offset of part p, element e: vmr +- K0 a
     };
     const int32_t wm0_32 = (int32_t)wm0;   // (32-bit: the SALU compares; operands < 2^31 rows)
     auto tri_step = [&](int64_t kt) -> TriStep {
@@ -1366,11 +1341,11 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
             t.so_dia = K0 * 16u * (uint32_t)sizeof(T);
             t.so_in = (uint32_t)kt * 128u;
 #pragma unroll
-            for (int pp = 0; pp < NPART; ++pp) {
-                uint32_t m = vdma[pp];
-                if (TRI == 3) m += __umul24(K0, adma8[pp]);
-                if (TRI == 4) m -= __umul24(K0, adma8[pp]);
-                t.md[pp] = m;
+            for (int pe = 0; pe < NPART * 2; ++pe) {
+                uint32_t m = vmr[pe];
+                if (TRI == 3) m += __umul24(K0, amr8[pe]);
+                if (TRI == 4) m -= __umul24(K0, amr8[pe]);
+                t.mr[pe] = m;
             }
         }
         return t;
@@ -1392,33 +1367,26 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
             // uniform class: control flow here (the per-element straddle loads of round 4) left the
             // compiler unable to count the prefetch ring's loads, and it waited for each one at once
             // (vmcnt(0)/(1) where the plain kernel waits with vmcnt(7))
-            // every class through the wave's LDS slot by LDS-DMA (asm: the compiler sees no VMEM
-            // in this loop, so nothing of its own waits on these copies; the consumer counts them).
-            // Constant offsets ride in soffset: an LDS-DMA's immediate offset moves its LDS
-            // destination as well as its source.
+            // two 8-B loads (inline asm: the compiler sees no VMEM in this loop, so it neither waits
+            // on them nor miscounts a ring whose classes differ; the consumer waits, counting them)
             const int c = i % FB, pp = i / FB;
-            const uint32_t m0v = mring0 + (uint32_t)slot * 1024u;
-            if (is_mir(ts_, c)) {   // mirrored: along the stored rows (vdma), read back transposed
-                asm volatile("s_mov_b32 m0, %0\n\t"
-                             "s_nop 0\n\t"
-                             "buffer_load_dwordx4 %1, %2, %3 offen lds"
-                             :
-                             : "s"(m0v), "v"(ts_.md[pp]), "s"(mrs4), "s"(ts_.so_mir + (uint32_t)(16 * c * (int)sizeof(T)))
-                             : "memory", "m0");
+            typedef T t2_t[2];
+            t2_t &dst = *reinterpret_cast<t2_t *>(&mv[slot]);
+            auto ld8 = [&](T &o, uint32_t vo, const u32x4_t &rs_, uint32_t so) {
+                asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen" : "=v"(o) : "v"(vo), "s"(rs_), "s"(so) : "memory");
+            };
+            if (is_mir(ts_, c)) {   // mirrored: down the stored rows, at the lane's own position
+                const uint32_t so_ = ts_.so_mir + (uint32_t)(16 * c * (int)sizeof(T));
+                ld8(dst[0], ts_.mr[2 * pp], mrs4, so_);
+                ld8(dst[1], ts_.mr[2 * pp + 1], mrs4, so_);
             } else if (c == ts_.cd) {   // the diagonal block, from the workspace
-                asm volatile("s_mov_b32 m0, %0\n\t"
-                             "s_nop 0\n\t"
-                             "buffer_load_dwordx4 %1, %2, %3 offen lds"
-                             :
-                             : "s"(m0v), "v"(vdiag), "s"(drs4), "s"(ts_.so_dia + (uint32_t)(16 * pp))
-                             : "memory", "m0");
-            } else {   // inside the triangle: the lane's own 16 B, as full storage
-                asm volatile("s_mov_b32 m0, %0\n\t"
-                             "s_nop 0\n\t"
-                             "buffer_load_dwordx4 %1, %2, %3 offen lds"
-                             :
-                             : "s"(m0v), "v"(voff[c]), "s"(mrs4), "s"(ts_.so_in + (uint32_t)(16 * pp))
-                             : "memory", "m0");
+                const uint32_t so_ = ts_.so_dia + (uint32_t)(16 * pp);
+                ld8(dst[0], vdiag, drs4, so_);
+                ld8(dst[1], vdiag, drs4, so_ + 8u);
+            } else {   // inside the triangle: the lane's own two values, as full storage
+                const uint32_t so_ = ts_.so_in + (uint32_t)(16 * pp);
+                ld8(dst[0], voff[c], mrs4, so_);
+                ld8(dst[1], voff[c], mrs4, so_ + 8u);
             }
             return;
         }
@@ -1522,7 +1490,6 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
         const TriStep t0 = tri_step(kt0);
 #pragma unroll
         for (int i = 0; i < PF; ++i) mload(i % NSLOT, CMAJOR ? seq_block(i) : i, kt0, t0);
-        if constexpr (TRI != 0) lds_read(yb[0], 0, is_mir(t0, 0));   // the first part-block's values
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
@@ -1580,28 +1547,13 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
                     if constexpr (TRI == 0) {
                         m = mv[i % NSLOT];
                     } else {
-                        // this part-block's values were read from LDS during the previous part-block
-                        // (yb[i & 1]); the read of the next one starts now, under this one's MFMAs
-                        T (&cur)[2] = yb[i & 1];
-                        if (c == 0) {
-                            // first part-block of a part: the generated fragments (gf, read just above)
-                            // complete with it, inside this wait, so the compiler puts no wait of its own
-                            // before the MFMAs -- its count cannot see the read issued below and would
-                            // wait for that too
-                            static_assert(FA == 4, "four generated fragments per part");
-                            asm volatile("s_waitcnt lgkmcnt(0)"
-                                         : "+v"(cur[0]), "+v"(cur[1]), "+v"(gf[0]), "+v"(gf[1]), "+v"(gf[2]), "+v"(gf[3])
-                                         :
-                                         : "memory");
-                        } else {
-                            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur[0]), "+v"(cur[1]) : : "memory");
-                        }
-                        if (i + 1 < NH) lds_read(yb[(i + 1) & 1], (i + 1) % NSLOT, is_mir(tsc, (i + 1) % FB));
-                        else lds_read(yb[(i + 1) & 1], (i + 1) % NSLOT, is_mir(tsn, 0));
-                        // (the read stays ahead of this part-block's MFMAs, in its own registers)
-                        __builtin_amdgcn_sched_barrier(0);
-                        m[0] = cur[0];
-                        m[1] = cur[1];
+                        // the part-block's two loads have landed once at most the 2 PF issued after
+                        // them are in flight (two per part-block, in order)
+                        typedef T t2_t[2];
+                        t2_t &src = *reinterpret_cast<t2_t *>(&mv[i % NSLOT]);
+                        asm volatile("s_waitcnt vmcnt(%2)" : "+v"(src[0]), "+v"(src[1]) : "n"(2 * PF) : "memory");
+                        m[0] = src[0];
+                        m[1] = src[1];
                     }
 #pragma unroll
                     for (int e = 0; e < PV; ++e)
@@ -1622,8 +1574,8 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
 
-    // the one-triangle copies the compiler cannot see: the last (clamped) ones land before the
-    // workgroup's LDS can be handed to another
+    // the one-triangle loads the compiler cannot see: the last (clamped) ones land before the
+    // registers they write are reused by the epilogue
     if constexpr (TRI != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     // split-K: alpha times this split's partial sum to partial[z]; the reduction adds them in order
@@ -2084,10 +2036,11 @@ static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
 }
 
 // The one-triangle operand streams by default (RBH_TRI_STREAMED, variants.hpp): skge_stream_kernel
-// with TRI, every part-block through the wave's LDS slot (mirrored ones transposed there), the
-// diagonal blocks from tri_diag_kernel's workspace. C5p (packed, d = 512, n = 16384): 4.31-4.32 ms
-// against 4.59-4.61 ms through the wide kernel's LDS transpose (round 4's streamed form with 8-B
-// loads per mirrored element: 4.85). The materialised-window option keeps the wide kernel.
+// with TRI, two 8-B loads per part-block into the register ring (mirrored ones down the stored rows),
+// the diagonal blocks from tri_diag_kernel's workspace. C5p (packed, d = 512, n = 16384): 4.25-4.26 ms
+// against 4.59-4.61 ms through the wide kernel's LDS transpose (round 4's streamed form with the same
+// 8-B loads, but compiler-visible behind branches: 4.85; through an LDS-DMA slot: 4.31-4.34). The
+// materialised-window option keeps the wide kernel.
 // the wide kernel instantiated for one-triangle operand p.tri (1-4): through LDS, or streamed
 template <int FAM, bool GX>
 static hipError_t launch_wide_tri(const GemmProblem &p, hipStream_t s) {

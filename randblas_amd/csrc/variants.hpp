@@ -20,7 +20,7 @@
 #define RBH_PF_TRI 7
 #endif
 // one-triangle symmetric operands (sketch_symmetric_triangle, packed A): 1 = the streamed kernel
-// (C5p 4.31-4.32 ms against 4.59-4.61 with 0), 0 = skge_wide_kernel's LDS transpose of the mirrored
+// (C5p 4.25-4.26 ms against 4.59-4.61 with 0), 0 = skge_wide_kernel's LDS transpose of the mirrored
 // tiles (the materialised-window option always takes it)
 #ifndef RBH_TRI_STREAMED
 #define RBH_TRI_STREAMED 1
