@@ -1169,6 +1169,7 @@ int sksy_overlapped(GemmProblem p, char layout, const T *dA, int64_t n, int64_t 
     p.C = W;
     p.ldc = p.M;
     p.beta = 0.0;
+    p.beside = 1;   // the check's waves need 32 registers a SIMD lane beside the GEMM's
     RBH_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
     RBH_HIP(hipEventRecord(fork, s));
     RBH_HIP(launch_gemm_t<T>(p, s));           // the sketch first: its workgroups take the CUs

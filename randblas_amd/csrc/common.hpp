@@ -64,6 +64,10 @@ struct GemmProblem {
     // s >= 2 = exactly s slices; materialise 1 = draw the operator window into a workspace first.
     int split_req;
     int materialise;
+    // 1: the call runs beside another kernel that needs 32 registers a SIMD lane (sketch_symmetric's
+    // overlapped check): the streamed f64 kernel keeps its 64 x 512 tiles (236 registers a wave)
+    // instead of the 32 x 1024 ones (256)
+    int beside;
 };
 
 // The kernel launch_gemm_* would run for a problem, and its split-K factor (rbh_plan).

@@ -1883,6 +1883,15 @@ static StreamGeom stream_geom(const GemmProblem &p) {
             const int sh = choose_split(t32, nk, 0);
             if (sh < s32 && t32 * sh >= wide * s32) return {32, 64, sh};
         }
+        // full unsplit grids: 32 x 1024 tiles (8 waves x 128 memory rows, the same 128 accumulator
+        // registers), each operator entry drawn per 1024 memory rows instead of 512 -- half the
+        // Philox/Box-Muller VALU per MFMA, which the MFMAs' hold on their SIMD's issue makes pay in
+        // full -- for twice the memory-operand loads per MFMA (VMEM, no VALU). Round 5, same box, two
+        // alternations: C2 7.66-7.68 ms = 91.1-91.3 % of the f64 peak against 7.97 (87.8 %) on 64 x 512,
+        // NS 15.30-15.31 against 15.91, C5's sketch 3.91 against 4.02 ms (PF 7; PF 3: C2 7.70-7.71).
+        // Round 4 had measured this shape slower (8.92-9.15 ms), before the scheduling barriers and
+        // the SGPR buffer resource of the streamed kernel.
+        if (s32 == 1 && !p.beside && ((gnO + 31) / 32) * ((mnO + 1023) / 1024) >= device_cus()) return {32, 128, 1};
         return {64, 64, s32};
     }
     const int64_t t64 = ((gnO + 63) / 64) * ((mnO + 1023) / 1024), t32 = ((gnO + 31) / 32) * ((mnO + 1023) / 1024);
@@ -1975,7 +1984,8 @@ template <typename T> constexpr int stream_pf() { return sizeof(T) == 8 ? RBH_PF
 template <typename T, int GK, int FAMILY, bool GX, int TRI = 0>
 static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
     const int64_t gnO = GX ? p.M : p.N, mnO = GX ? p.N : p.M;
-    const StreamGeom gm = stream_geom<T>(p);
+    StreamGeom gm = stream_geom<T>(p);
+    if (TRI && gm.mw == 128) gm = StreamGeom{64, 64, gm.split};   // one-triangle operands: 64 x 512 tiles
     const int64_t nb = ((gnO + gm.bg - 1) / gm.bg) * ((mnO + 8 * gm.mw - 1) / (8 * gm.mw));
     if (nb <= 0) return hipSuccess;
     const int split = gm.split;
@@ -2005,8 +2015,10 @@ static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
     timing_begin(s);
     const dim3 grid((unsigned)(nb * split));
     constexpr int PF = TRI ? RBH_PF_TRI : stream_pf<T>();
-    if constexpr (sizeof(T) == 8) {   // 64 x 512 tiles (64 x 1024 would take 256 accumulator registers)
-        if (!TRI && gm.bg == 32) {   // small grids: 32 x 512 tiles (stream_geom), split K
+    if constexpr (sizeof(T) == 8) {   // 32 x 1024 or 64 x 512 tiles (64 x 1024 would take 256 accumulator registers)
+        if (!TRI && gm.mw == 128) {   // full unsplit grids: 32 x 1024 tiles (stream_geom)
+            hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, PF, 32, 128, 0>), grid, dim3(512), 0, s, q);
+        } else if (!TRI && gm.bg == 32) {   // small grids: 32 x 512 tiles (stream_geom), split K
             hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, 3, 32, 64, 0>), grid, dim3(512), 0, s, q);
         } else if (split > 1) hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, PF, 64, 64, TRI>), grid, dim3(512), 0, s, q);
         else hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, PF, 64, 64, TRI>), grid, dim3(512), 0, s, q);

@@ -8,8 +8,9 @@
 #pragma once
 
 // ---- skge_dense.hip: the streamed GEMM (skge_stream_kernel) ---------------------------------
-// memory-operand prefetch depth, in part-blocks ahead of their use: f64 7 (C2 7.97-7.98 ms against
-// 7.99-8.02 with 3), f32 3 (C4 4.08-4.11 against 4.18-4.20 with 1), the one-triangle forms 7
+// memory-operand prefetch depth, in part-blocks ahead of their use: f64 7 (64 x 512 tiles: C2 7.97-7.98
+// ms against 7.99-8.02 with 3; 32 x 1024 tiles: C2 7.66-7.68 against 7.70-7.71 with 3, C5 3.91 against
+// 4.02-4.08), f32 3 (C4 4.08-4.11 against 4.18-4.20 with 1), the one-triangle forms 7
 #ifndef RBH_PF64
 #define RBH_PF64 7
 #endif

@@ -356,3 +356,17 @@ def test_sketch_symmetric_check_positions(cuda, n, lda, layout):
             rb.sketch_symmetric_left(layout, d, n, 1.0, S, dev(stored(Mp), cuda), lda, 0.0, B,
                                      d if layout == "C" else n)
         assert np.array_equal(host(B), B0), (i, j)
+
+
+def test_sksy_tri_ragged_full_grid(cuda):
+    """A one-triangle call whose grid is full and unsplit -- where the plain kernel takes 32 x 1024
+    tiles -- with ragged tile edges (d = 1650: 52 x 5 = 260 such tiles; 26 x 9 of 64 x 512): the
+    one-triangle kernel keeps its 64 x 512 tiles and their count, bitwise the full-storage product."""
+    d, n = 1650, 4112
+    M = sym_full(n, 21)
+    ref, S, ldb = full_sketch(cuda, "L", "C", d, n, M)
+    B = torch.zeros(d * n, dtype=torch.float64, device=cuda)
+    rb.sketch_symmetric_tri("C", "L", "U", "P", d, n, 0.75, S, dev(packed(M, "C", "U"), cuda), 0, 0.0, B, ldb,
+                            ro_s=2, co_s=4)
+    got = host(B)
+    assert np.array_equal(got.view(np.uint64), ref.view(np.uint64)), f"{np.sum(got != ref)} differ"
