@@ -82,6 +82,7 @@ enum PlanKernel : int {
     PLAN_SYMMETRIZE = 7,  // one-triangle operand expanded into a workspace, then the plain kernels
     PLAN_STREAM = 8,      // skge_stream_kernel (the wide kernels' sums; f64 64 x 512, f32 32 / 64 x 1024)
     PLAN_STREAM_TRI = 9,  // skge_stream_kernel with a one-triangle symmetric operand (f64)
+    PLAN_STREAM_T = 10,   // skge_stream_kernel<TRI 5>: memory operand contiguous along o (f64)
 };
 struct GemmPlan {
     int kernel;

@@ -1209,7 +1209,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     constexpr int NH = NPART * FB;                        // part-blocks of a step (part FB + c)
     constexpr int NSLOT = PF + 1;                         // register slots of the memory prefetch ring
     static_assert(NH % NSLOT == 0, "a part-block's slot must not depend on the step");
-    static_assert(TRI == 0 || (NPART == 2 && sizeof(T) == 8), "one-triangle operands: f64 64-row tiles (lane pairs)");
+    static_assert(TRI == 0 || sizeof(T) == 8, "one-triangle operands: f64");
     // consumption order of a step's part-blocks: part-major (part p of every block, then part p + 1)
     // or block-major (CMAJOR: both parts of block c, then block c + 1); every accumulator sees the same
     // k order either way (its block's parts in turn), so the sums are the same bits
@@ -1265,13 +1265,17 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     // the stored triangle (loads past it return 0): a mirrored pair load (below) of a row past the
     // operand's last one reads past its stored row, for an output that is discarded.
     constexpr bool TKLE = TRI == 1 || TRI == 3;
-    const uint32_t tso = (uint32_t)mop.so, tn = (uint32_t)p.tri_n;
+    // TRI 5: a transposed memory operand (element (o, k) at k sk + o: every part-block "mirrored", read
+    // down the stored rows k at the lane's position o; no triangle, no diagonal blocks)
+    const uint32_t tso = (uint32_t)(TRI == 5 ? mop.sk : mop.so), tn = (uint32_t)p.tri_n;
     auto rowbase = [&](uint32_t a) -> uint32_t {
         if (TRI == 3) return a * (a + 1) / 2;
         if (TRI == 4) return a * tn - a * (a + 1) / 2;
         return a * tso;
     };
-    const int32_t mrange = TRI == 0 ? -1 : (int32_t)((TRI <= 2 ? (tn - 1) * tso + tn : tn * (tn + 1) / 2) * (uint32_t)sizeof(T));
+    const int32_t mrange = TRI == 0 ? -1
+                         : TRI == 5 ? (int32_t)((((uint32_t)p.K - 1) * tso + (uint32_t)mnO) * (uint32_t)sizeof(T))
+                                    : (int32_t)((TRI <= 2 ? (tn - 1) * tso + tn : tn * (tn + 1) / 2) * (uint32_t)sizeof(T));
     const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(uintptr_t)(((uint64_t)mb_hi << 32) | mb_lo), (short)0, mrange, 0x00020000);
     uint32_t voff[FB];
@@ -1290,12 +1294,12 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     // loads in flight after a part-block's is exact. The values are moved, not computed: the MFMA sums
     // are full storage's bits. Byte offset: rowbase(K0 + a) + o = rowbase(K0) (uniform, soffset) + a
     // lane constant (vmr) + K0 a (packed lower) / - K0 a (packed upper) per step + 128 c (immediate).
-    uint32_t vmr[TRI ? NPART * 2 : 1], amr8[TRI ? NPART * 2 : 1];
+    uint32_t vmr[TRI ? VPL : 1], amr8[TRI ? VPL : 1];
     if constexpr (TRI != 0) {
 #pragma unroll
-        for (int pe = 0; pe < NPART * 2; ++pe) {
-            const uint32_t a = (uint32_t)(VPL * g + PV * (pe >> 1) + (pe & 1));
-            const uint32_t lane_part = TRI <= 2 ? a * tso : (TRI == 3 ? a * (a + 1) / 2 : a * tn - a * (a + 1) / 2);
+        for (int pe = 0; pe < VPL; ++pe) {   // value pe of the lane's VPL: part pe / PV, element pe % PV
+            const uint32_t a = (uint32_t)(VPL * g + pe);
+            const uint32_t lane_part = (TRI <= 2 || TRI == 5) ? a * tso : (TRI == 3 ? a * (a + 1) / 2 : a * tn - a * (a + 1) / 2);
             vmr[pe] = (lane_part + (uint32_t)(wm0 < mnO ? wm0 : 0) + (uint32_t)r) * (uint32_t)sizeof(T);
             amr8[pe] = a * (uint32_t)sizeof(T);
         }
@@ -1329,7 +1333,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
         uint32_t so_mir;     // rowbase(K0) bytes
         uint32_t so_dia;     // K0 * 128: block K0 / 16 of the diagonal workspace
         uint32_t so_in;      // kt * 128
-        uint32_t mr[NPART * 2];   // mirrored load offset of part p, element e: vmr +- K0 a
+        uint32_t mr[VPL];         // mirrored load offset of part p, element e (index PV p + e): vmr +- K0 a
     };
     const int32_t wm0_32 = (int32_t)wm0;   // (32-bit: the SALU compares; operands < 2^31 rows)
     auto tri_step = [&](int64_t kt) -> TriStep {
@@ -1341,7 +1345,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
             t.so_dia = K0 * 16u * (uint32_t)sizeof(T);
             t.so_in = (uint32_t)kt * 128u;
 #pragma unroll
-            for (int pe = 0; pe < NPART * 2; ++pe) {
+            for (int pe = 0; pe < VPL; ++pe) {
                 uint32_t m = vmr[pe];
                 if (TRI == 3) m += __umul24(K0, amr8[pe]);
                 if (TRI == 4) m -= __umul24(K0, amr8[pe]);
@@ -1350,7 +1354,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
         }
         return t;
     };
-    auto is_mir = [&](const TriStep &t, int c) -> bool { return TKLE ? c < t.cd : c > t.cd; };
+    auto is_mir = [&](const TriStep &t, int c) -> bool { return TRI == 5 || (TKLE ? c < t.cd : c > t.cd); };
     // in-triangle bases less their immediate 128 c (the immediate adds it back)
     uint32_t voffi[TRI ? FB : 1];
     if (TRI) {
@@ -1367,26 +1371,26 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
             // uniform class: control flow here (the per-element straddle loads of round 4) left the
             // compiler unable to count the prefetch ring's loads, and it waited for each one at once
             // (vmcnt(0)/(1) where the plain kernel waits with vmcnt(7))
-            // two 8-B loads (inline asm: the compiler sees no VMEM in this loop, so it neither waits
+            // PV 8-B loads (inline asm: the compiler sees no VMEM in this loop, so it neither waits
             // on them nor miscounts a ring whose classes differ; the consumer waits, counting them)
             const int c = i % FB, pp = i / FB;
-            typedef T t2_t[2];
-            t2_t &dst = *reinterpret_cast<t2_t *>(&mv[slot]);
+            typedef T tv_t[PV];
+            tv_t &dst = *reinterpret_cast<tv_t *>(&mv[slot]);
             auto ld8 = [&](T &o, uint32_t vo, const u32x4_t &rs_, uint32_t so) {
                 asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen" : "=v"(o) : "v"(vo), "s"(rs_), "s"(so) : "memory");
             };
             if (is_mir(ts_, c)) {   // mirrored: down the stored rows, at the lane's own position
                 const uint32_t so_ = ts_.so_mir + (uint32_t)(16 * c * (int)sizeof(T));
-                ld8(dst[0], ts_.mr[2 * pp], mrs4, so_);
-                ld8(dst[1], ts_.mr[2 * pp + 1], mrs4, so_);
+#pragma unroll
+                for (int e = 0; e < PV; ++e) ld8(dst[e], ts_.mr[PV * pp + e], mrs4, so_);
             } else if (c == ts_.cd) {   // the diagonal block, from the workspace
-                const uint32_t so_ = ts_.so_dia + (uint32_t)(16 * pp);
-                ld8(dst[0], vdiag, drs4, so_);
-                ld8(dst[1], vdiag, drs4, so_ + 8u);
-            } else {   // inside the triangle: the lane's own two values, as full storage
-                const uint32_t so_ = ts_.so_in + (uint32_t)(16 * pp);
-                ld8(dst[0], voff[c], mrs4, so_);
-                ld8(dst[1], voff[c], mrs4, so_ + 8u);
+                const uint32_t so_ = ts_.so_dia + (uint32_t)(8 * PV * pp);
+#pragma unroll
+                for (int e = 0; e < PV; ++e) ld8(dst[e], vdiag, drs4, so_ + 8u * e);
+            } else {   // inside the triangle: the lane's own values, as full storage
+                const uint32_t so_ = ts_.so_in + (uint32_t)(8 * PV * pp);
+#pragma unroll
+                for (int e = 0; e < PV; ++e) ld8(dst[e], voff[c], mrs4, so_ + 8u * e);
             }
             return;
         }
@@ -1547,13 +1551,17 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
                     if constexpr (TRI == 0) {
                         m = mv[i % NSLOT];
                     } else {
-                        // the part-block's two loads have landed once at most the 2 PF issued after
-                        // them are in flight (two per part-block, in order)
-                        typedef T t2_t[2];
-                        t2_t &src = *reinterpret_cast<t2_t *>(&mv[i % NSLOT]);
-                        asm volatile("s_waitcnt vmcnt(%2)" : "+v"(src[0]), "+v"(src[1]) : "n"(2 * PF) : "memory");
-                        m[0] = src[0];
-                        m[1] = src[1];
+                        // the part-block's PV loads have landed once at most the PV PF issued after
+                        // them are in flight (PV per part-block, in order)
+                        typedef T tv_t[PV];
+                        tv_t &src = *reinterpret_cast<tv_t *>(&mv[i % NSLOT]);
+                        if constexpr (PV == 2)
+                            asm volatile("s_waitcnt vmcnt(%2)" : "+v"(src[0]), "+v"(src[1]) : "n"(PV * PF) : "memory");
+                        else
+                            asm volatile("s_waitcnt vmcnt(%4)" : "+v"(src[0]), "+v"(src[1]), "+v"(src[2]), "+v"(src[3])
+                                         : "n"(PV * PF) : "memory");
+#pragma unroll
+                        for (int e = 0; e < PV; ++e) m[e] = src[e];
                     }
 #pragma unroll
                     for (int e = 0; e < PV; ++e)
@@ -1985,7 +1993,9 @@ template <typename T, int GK, int FAMILY, bool GX, int TRI = 0>
 static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
     const int64_t gnO = GX ? p.M : p.N, mnO = GX ? p.N : p.M;
     StreamGeom gm = stream_geom<T>(p);
-    if (TRI && gm.mw == 128) gm = StreamGeom{64, 64, gm.split};   // one-triangle operands: 64 x 512 tiles
+    // one-triangle operands: the full-storage call's tiles (RBH_TRI_WIDE), else 64 x 512 (the split is
+    // the same either way, so the sums are full storage's bits)
+    if (TRI && TRI != 5 && !RBH_TRI_WIDE) gm = StreamGeom{64, 64, gm.split};
     const int64_t nb = ((gnO + gm.bg - 1) / gm.bg) * ((mnO + 8 * gm.mw - 1) / (8 * gm.mw));
     if (nb <= 0) return hipSuccess;
     const int split = gm.split;
@@ -1998,7 +2008,7 @@ static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
         if (e != hipSuccess) return e;
     }
     void *diag = nullptr;
-    if constexpr (TRI != 0) {   // the operand's diagonal blocks, both triangles (tri_diag_kernel)
+    if constexpr (TRI != 0 && TRI != 5) {   // the operand's diagonal blocks, both triangles (tri_diag_kernel)
         const MemOperand &mo = GX ? p.ym : p.xm;
         e = ws_alloc(&diag, sizeof(double) * 256 * (size_t)(p.tri_n / 16), s);
         if (e == hipSuccess && p.tri_n >= 16)
@@ -2015,11 +2025,12 @@ static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
     timing_begin(s);
     const dim3 grid((unsigned)(nb * split));
     constexpr int PF = TRI ? RBH_PF_TRI : stream_pf<T>();
+    constexpr int PF32 = TRI ? RBH_PF_TRI32 : stream_pf<T>();   // 32-row tiles
     if constexpr (sizeof(T) == 8) {   // 32 x 1024 or 64 x 512 tiles (64 x 1024 would take 256 accumulator registers)
-        if (!TRI && gm.mw == 128) {   // full unsplit grids: 32 x 1024 tiles (stream_geom)
-            hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, PF, 32, 128, 0>), grid, dim3(512), 0, s, q);
-        } else if (!TRI && gm.bg == 32) {   // small grids: 32 x 512 tiles (stream_geom), split K
-            hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, 3, 32, 64, 0>), grid, dim3(512), 0, s, q);
+        if (gm.mw == 128) {   // full unsplit grids: 32 x 1024 tiles (stream_geom)
+            hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, PF32, 32, 128, TRI>), grid, dim3(512), 0, s, q);
+        } else if (gm.bg == 32) {   // small grids: 32 x 512 tiles (stream_geom), split K
+            hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, 3, 32, 64, TRI>), grid, dim3(512), 0, s, q);
         } else if (split > 1) hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, PF, 64, 64, TRI>), grid, dim3(512), 0, s, q);
         else hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, PF, 64, 64, TRI>), grid, dim3(512), 0, s, q);
     } else if (gm.bg == 64) {
@@ -2103,6 +2114,23 @@ static hipError_t launch_gemm_tri(const GemmProblem &p, hipStream_t s) {
     return unif ? launch_wide_tri<rb::UNIFORM, false>(p, s) : launch_wide_tri<rb::GAUSSIAN, false>(p, s);
 }
 
+// Memory operand contiguous along its outer index (so == 1, k stride sk: A of a RowMajor left or a
+// ColMajor right sketch): skge_stream_kernel<TRI 5> reads it down the stored rows k, 16 lanes of a
+// row group over 128 contiguous bytes, as the one-triangle kernel's mirrored blocks (f64; the generic
+// kernel otherwise: 61 % of the f64 peak at d = 1024, m = n = 16384). The values are moved, not
+// computed, so the sums are those of the same problem with the operand stored along k.
+template <typename T>
+static bool stream_t_ok(const GemmProblem &p) {
+    if (sizeof(T) != 8 || p.tri || p.materialise || (p.xkind == MEM) == (p.ykind == MEM)) return false;
+    const bool gx = p.xkind != MEM;
+    const GenOperand &g = gx ? p.xg : p.yg;
+    const MemOperand &m = gx ? p.ym : p.xm;
+    const int64_t mnO = gx ? p.N : p.M;
+    if ((g.pc0 & 3) || p.K % BK || m.so != 1 || m.sk <= 1) return false;
+    // 32-bit byte offsets over the operand's K stored rows
+    return ((p.K - 1) * m.sk + mnO) * (int64_t)sizeof(T) < ((int64_t)1 << 32);
+}
+
 // Which kernel launch_gemm runs for p, with its tiles and split (the same tests, in the same order).
 template <typename T>
 static GemmPlan plan_gemm(const GemmProblem &p) {
@@ -2131,11 +2159,11 @@ static GemmPlan plan_gemm(const GemmProblem &p) {
         pl.kernel = RBH_TRI_STREAMED && !p.materialise ? PLAN_STREAM_TRI : PLAN_WIDE_TRI;   // as launch_wide_tri
         pl.tiles = wide_tiles();
         pl.splitk = stream_geom<T>(p).split;   // as launch_wide
-    } else if (stream_ok<T>(p)) {
+    } else if (stream_ok<T>(p) || stream_t_ok<T>(p)) {
         const bool gx = p.xkind != MEM;
         const int64_t gnO = gx ? p.M : p.N, mnO = gx ? p.N : p.M;
         const StreamGeom gm = stream_geom<T>(p);   // as launch_stream
-        pl.kernel = PLAN_STREAM;
+        pl.kernel = stream_ok<T>(p) ? PLAN_STREAM : PLAN_STREAM_T;
         pl.tiles = ((gnO + gm.bg - 1) / gm.bg) * ((mnO + 8 * gm.mw - 1) / (8 * gm.mw));
         pl.splitk = gm.split;
     } else if (wide_ok<T>(p)) {
@@ -2179,6 +2207,17 @@ static hipError_t launch_gemm(const GemmProblem &p, hipStream_t s) {
         if (p.ykind == GEN_OK) { RBH_STREAM_L(GEN_OK, false); }
         if (p.ykind == GEN_OO) { RBH_STREAM_L(GEN_OO, false); }
 #undef RBH_STREAM_L
+    }
+    if constexpr (sizeof(T) == 8) {
+        if (kernel == PLAN_STREAM_T) {
+#define RBH_STREAM_T(GK, GX)                                                                   \
+    return unif ? launch_stream<T, GK, rb::UNIFORM, GX, 5>(p, s) : launch_stream<T, GK, rb::GAUSSIAN, GX, 5>(p, s)
+            if (p.xkind == GEN_OK) { RBH_STREAM_T(GEN_OK, true); }
+            if (p.xkind == GEN_OO) { RBH_STREAM_T(GEN_OO, true); }
+            if (p.ykind == GEN_OK) { RBH_STREAM_T(GEN_OK, false); }
+            if (p.ykind == GEN_OO) { RBH_STREAM_T(GEN_OO, false); }
+#undef RBH_STREAM_T
+        }
     }
     if (kernel == PLAN_WIDE) {
 #define RBH_WIDE_L(GK, GX)                                                                     \

@@ -23,6 +23,18 @@
 // one-triangle symmetric operands (sketch_symmetric_triangle, packed A): 1 = the streamed kernel
 // (C5p 4.25-4.26 ms against 4.59-4.61 with 0), 0 = skge_wide_kernel's LDS transpose of the mirrored
 // tiles (the materialised-window option always takes it)
+// one-triangle operands on the full-storage call's tile shape (1: 32 x 1024 tiles for full unsplit
+// grids, 32 x 512 for small split grids; 0: always 64 x 512), and the prefetch depth of the 32-row
+// forms (one-triangle and transposed operands: their part-blocks are four 8-B loads). With 1, C5p took
+// 5.50-5.55 ms against 4.26-4.32 (tools/time_tri.py, same box): blocks inside the triangle as four
+// 8-B loads a lane touch 16 cache lines per instruction (64 a part-block, twice full storage's) and
+// run at half speed (all-inside ablation 7.1 ms; all-mirrored 3.87-3.95 ms = 89-90 % of the f64 peak)
+#ifndef RBH_TRI_WIDE
+#define RBH_TRI_WIDE 0
+#endif
+#ifndef RBH_PF_TRI32
+#define RBH_PF_TRI32 3
+#endif
 #ifndef RBH_TRI_STREAMED
 #define RBH_TRI_STREAMED 1
 #endif

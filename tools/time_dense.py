@@ -22,17 +22,30 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--splitk", type=int, default=0, help="rbh_options.splitk (0 = the library's choice)")
+    ap.add_argument("--layout", default="C", choices=["C", "R"])
+    ap.add_argument("--side", default="left", choices=["left", "right"], help="right: B (m x d) = A (m x n) S (n x d)")
+    ap.add_argument("--opS", default="N", choices=["N", "T"])
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     tdt = torch.float64 if a.dtype == "f64" else torch.float32
     A = torch.empty(a.m * a.n, dtype=tdt, device=dev)
     rb.fill_dense("C", rb.DenseDist(a.m, a.n), a.m, a.n, 0, 0, A, rb.RNGState(99))
-    S = rb.DenseSkOp(rb.DenseDist(a.d, a.m), rb.RNGState(0))
-    B = torch.empty(a.d * a.n, dtype=tdt, device=dev)
+    col = a.layout == "C"
+    if a.side == "left":   # B (d x n) = op(S) (d x m) A (m x n)
+        S = rb.DenseSkOp(rb.DenseDist(a.d, a.m) if a.opS == "N" else rb.DenseDist(a.m, a.d), rb.RNGState(0))
+        lda, ldb = (a.m, a.d) if col else (a.n, a.n)
+        B = torch.empty(a.d * a.n, dtype=tdt, device=dev)
+    else:                  # B (m x d) = A (m x n) op(S) (n x d)
+        S = rb.DenseSkOp(rb.DenseDist(a.n, a.d) if a.opS == "N" else rb.DenseDist(a.d, a.n), rb.RNGState(0))
+        lda, ldb = (a.m, a.m) if col else (a.n, a.d)
+        B = torch.empty(a.m * a.d, dtype=tdt, device=dev)
     opts = rb.Options(splitk=a.splitk)
 
     def call():
-        rb.sketch_general_left("C", "N", "N", a.d, a.n, a.m, 1.0, S, A, a.m, 0.0, B, a.d, options=opts)
+        if a.side == "left":
+            rb.sketch_general_left(a.layout, a.opS, "N", a.d, a.n, a.m, 1.0, S, A, lda, 0.0, B, ldb, options=opts)
+        else:
+            rb.sketch_general_right(a.layout, "N", a.opS, a.m, a.d, a.n, 1.0, A, lda, S, 0.0, B, ldb, options=opts)
 
     for _ in range(a.warmup):
         call()
@@ -44,12 +57,13 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.reps
-    plan = rb.plan_left("C", "N", "N", a.d, a.n, a.m, S, A, a.m, a.d, dtype=a.dtype, options=opts)
+    plan = rb.plan_left(a.layout, a.opS, "N", a.d, a.n, a.m, S, A, lda, ldb, dtype=a.dtype, options=opts) if a.side == "left" else None
     flops = 2.0 * a.d * a.m * a.n
     peak = 78.6e12 if a.dtype == "f64" else 157.3e12
-    print(json.dumps({"dtype": a.dtype, "d": a.d, "m": a.m, "n": a.n, "ms": ms, "tflops": flops / ms / 1e9,
-                      "frac": flops / ms / 1e-3 / peak, "plan": plan.kernel, "tiles": plan.tiles,
-                      "splitk": plan.splitk}))
+    print(json.dumps({"dtype": a.dtype, "d": a.d, "m": a.m, "n": a.n, "layout": a.layout, "side": a.side, "opS": a.opS,
+                      "ms": ms, "tflops": flops / ms / 1e9, "frac": flops / ms / 1e-3 / peak,
+                      "plan": plan.kernel if plan else None, "tiles": plan.tiles if plan else None,
+                      "splitk": plan.splitk if plan else None}))
 
 
 if __name__ == "__main__":
