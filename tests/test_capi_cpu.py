@@ -147,8 +147,11 @@ def test_plan_options_fix_the_split():
     assert _plan(128, 4096, 4096, opts=rb.Options(splitk=3)) == rb.Plan("stream", 3, 16, 48)
     assert _plan(1024, 16384, 16384, opts=rb.Options(splitk=2)).splitk == 2
     # RowMajor A with lda = n is contiguous along the output columns, not along the contracted
-    # index: the generic kernel (scalar loads along the outer index)
-    assert _plan(1024, 16384, 16384, layout="R").kernel == "generic"
+    # index: f64 streams it down its stored rows (stream_t, the full-grid 32 x 1024 tiles); f32 and
+    # an operand past 32-bit byte offsets take the generic kernel (scalar loads along the outer index)
+    assert _plan(1024, 16384, 16384, layout="R") == rb.Plan("stream_t", 1, 512, 512)
+    assert _plan(1024, 16384, 16384, layout="R", dtype="f32").kernel == "generic"
+    assert _plan(1024, 32768, 32768, layout="R").kernel == "generic"
     # the materialised window: the 64 x 512 kernels that load it (the same sums)
     assert _plan(1024, 16384, 16384, opts=rb.Options(materialise=True)).kernel == "wide"
     # (the f32 materialised kernel takes the streamed kernel's split: the same bits)
