@@ -1189,6 +1189,24 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
 // once. f32: C4 4.37 -> 4.03 ms (80.0 -> 86.7 % of the f32 peak, same box, two alternations), L2-miss
 // bytes 9.3-9.7 -> 4.7 GB per launch; d = 1024, m = n = 16384: 74.5 -> 80.5 %. f64 (block-major):
 // C2 8.005-8.011 -> 7.976 ms (profiles/r04/ab_sched_barrier.txt).
+// s_waitcnt vmcnt(N) for the one-triangle / transposed ring, then vm_fence: the ring registers as
+// in/out operands of one empty asm after the wait, which the MFMAs read (as "+v" operands of the wait
+// itself they must not differ between paths: a wait whose count was picked by branches got its own
+// registers per branch, and the compiler copied the ring into them ahead of the wait, i.e. while the
+// loads were in flight)
+template <int N>
+__device__ __forceinline__ void vm_wait_n() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+template <typename T>
+__device__ __forceinline__ void vm_fence(T (&s)[2]) { asm volatile("" : "+v"(s[0]), "+v"(s[1])::"memory"); }
+template <typename T>
+__device__ __forceinline__ void vm_fence(T (&s)[4]) {
+    asm volatile("" : "+v"(s[0]), "+v"(s[1]), "+v"(s[2]), "+v"(s[3])::"memory");
+}
+template <typename T>
+__device__ __forceinline__ void vm_fence(T (&s)[8]) {
+    asm volatile("" : "+v"(s[0]), "+v"(s[1]), "+v"(s[2]), "+v"(s[3]), "+v"(s[4]), "+v"(s[5]), "+v"(s[6]), "+v"(s[7])::"memory");
+}
+
 template <typename T, int GK, int FAMILY, bool GX, bool SPLIT, int PF, int BG, int MW, int TRI = 0>
 __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     constexpr int KS = 128 / (int)sizeof(T);              // k per step
@@ -1209,7 +1227,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     constexpr int NH = NPART * FB;                        // part-blocks of a step (part FB + c)
     constexpr int NSLOT = PF + 1;                         // register slots of the memory prefetch ring
     static_assert(NH % NSLOT == 0, "a part-block's slot must not depend on the step");
-    static_assert(TRI == 0 || sizeof(T) == 8, "one-triangle operands: f64");
+    static_assert(TRI == 0 || TRI == 5 || sizeof(T) == 8, "one-triangle operands: f64");
     // consumption order of a step's part-blocks: part-major (part p of every block, then part p + 1)
     // or block-major (CMAJOR: both parts of block c, then block c + 1); every accumulator sees the same
     // k order either way (its block's parts in turn), so the sums are the same bits
@@ -1371,18 +1389,32 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
             // uniform class: control flow here (the per-element straddle loads of round 4) left the
             // compiler unable to count the prefetch ring's loads, and it waited for each one at once
             // (vmcnt(0)/(1) where the plain kernel waits with vmcnt(7))
-            // PV 8-B loads (inline asm: the compiler sees no VMEM in this loop, so it neither waits
-            // on them nor miscounts a ring whose classes differ; the consumer waits, counting them)
+            // PV one-value loads whatever the class (inline asm: the compiler sees no VMEM in this
+            // loop, so it neither waits on them nor miscounts a ring whose classes differ; the
+            // consumer waits, counting them). (Round 5: the in-triangle and diagonal part-blocks as
+            // 16-B loads, with the consumer's count picked per class by uniform branches, took C5p
+            // 4.27 -> 4.89 ms: the branches cost more than the loads saved.)
             const int c = i % FB, pp = i / FB;
             typedef T tv_t[PV];
             tv_t &dst = *reinterpret_cast<tv_t *>(&mv[slot]);
-            auto ld8 = [&](T &o, uint32_t vo, const u32x4_t &rs_, uint32_t so) {
-                asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen" : "=v"(o) : "v"(vo), "s"(rs_), "s"(so) : "memory");
+            auto ld8 = [&](T &o, uint32_t vo, const u32x4_t &rs_, uint32_t so) {   // one value
+                if constexpr (sizeof(T) == 8)
+                    asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen" : "=v"(o) : "v"(vo), "s"(rs_), "s"(so) : "memory");
+                else
+                    asm volatile("buffer_load_dword %0, %1, %2, %3 offen" : "=v"(o) : "v"(vo), "s"(rs_), "s"(so) : "memory");
             };
             if (is_mir(ts_, c)) {   // mirrored: down the stored rows, at the lane's own position
                 const uint32_t so_ = ts_.so_mir + (uint32_t)(16 * c * (int)sizeof(T));
+                // stored rows at a fixed stride (full storage, TRI 1 / 2 / 5): value pe's row offset
+                // pe tso is uniform (soffset), one offset VGPR for all; packed rows: one per value
+                constexpr bool LIN = TRI == 1 || TRI == 2 || TRI == 5;
 #pragma unroll
-                for (int e = 0; e < PV; ++e) ld8(dst[e], ts_.mr[PV * pp + e], mrs4, so_);
+                for (int e = 0; e < PV; ++e) {
+                    const int pe = PV * pp + e;
+                    if (LIN) ld8(dst[e], ts_.mr[0], mrs4, so_ + (uint32_t)pe * tso * (uint32_t)sizeof(T));
+                    else ld8(dst[e], ts_.mr[pe], mrs4, so_);
+                }
+            } else if constexpr (TRI == 5) {
             } else if (c == ts_.cd) {   // the diagonal block, from the workspace
                 const uint32_t so_ = ts_.so_dia + (uint32_t)(8 * PV * pp);
 #pragma unroll
@@ -1552,14 +1584,12 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
                         m = mv[i % NSLOT];
                     } else {
                         // the part-block's PV loads have landed once at most the PV PF issued after
-                        // them are in flight (PV per part-block, in order)
+                        // them are in flight (PV per part-block, in order); then the ring registers
+                        // pass through one empty asm the MFMAs read, so nothing reads them earlier
                         typedef T tv_t[PV];
                         tv_t &src = *reinterpret_cast<tv_t *>(&mv[i % NSLOT]);
-                        if constexpr (PV == 2)
-                            asm volatile("s_waitcnt vmcnt(%2)" : "+v"(src[0]), "+v"(src[1]) : "n"(PV * PF) : "memory");
-                        else
-                            asm volatile("s_waitcnt vmcnt(%4)" : "+v"(src[0]), "+v"(src[1]), "+v"(src[2]), "+v"(src[3])
-                                         : "n"(PV * PF) : "memory");
+                        vm_wait_n<PV * PF>();
+                        vm_fence(src);
 #pragma unroll
                         for (int e = 0; e < PV; ++e) m[e] = src[e];
                     }
@@ -2024,7 +2054,7 @@ static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
     }
     timing_begin(s);
     const dim3 grid((unsigned)(nb * split));
-    constexpr int PF = TRI ? RBH_PF_TRI : stream_pf<T>();
+    constexpr int PF = (TRI && TRI != 5) ? RBH_PF_TRI : stream_pf<T>();
     constexpr int PF32 = TRI ? RBH_PF_TRI32 : stream_pf<T>();   // 32-row tiles
     if constexpr (sizeof(T) == 8) {   // 32 x 1024 or 64 x 512 tiles (64 x 1024 would take 256 accumulator registers)
         if (gm.mw == 128) {   // full unsplit grids: 32 x 1024 tiles (stream_geom)
@@ -2034,11 +2064,11 @@ static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
         } else if (split > 1) hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, PF, 64, 64, TRI>), grid, dim3(512), 0, s, q);
         else hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, PF, 64, 64, TRI>), grid, dim3(512), 0, s, q);
     } else if (gm.bg == 64) {
-        if (split > 1) hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, PF, 64, 128>), grid, dim3(512), 0, s, q);
-        else hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, PF, 64, 128>), grid, dim3(512), 0, s, q);
+        if (split > 1) hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, PF, 64, 128, TRI>), grid, dim3(512), 0, s, q);
+        else hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, PF, 64, 128, TRI>), grid, dim3(512), 0, s, q);
     } else {
-        if (split > 1) hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, PF, 32, 128>), grid, dim3(512), 0, s, q);
-        else hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, PF, 32, 128>), grid, dim3(512), 0, s, q);
+        if (split > 1) hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, PF, 32, 128, TRI>), grid, dim3(512), 0, s, q);
+        else hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, PF, 32, 128, TRI>), grid, dim3(512), 0, s, q);
     }
     e = hipGetLastError();
     if (split > 1 && e == hipSuccess) {
@@ -2121,12 +2151,12 @@ static hipError_t launch_gemm_tri(const GemmProblem &p, hipStream_t s) {
 // computed, so the sums are those of the same problem with the operand stored along k.
 template <typename T>
 static bool stream_t_ok(const GemmProblem &p) {
-    if (sizeof(T) != 8 || p.tri || p.materialise || (p.xkind == MEM) == (p.ykind == MEM)) return false;
+    if (p.tri || p.materialise || (p.xkind == MEM) == (p.ykind == MEM)) return false;
     const bool gx = p.xkind != MEM;
     const GenOperand &g = gx ? p.xg : p.yg;
     const MemOperand &m = gx ? p.ym : p.xm;
     const int64_t mnO = gx ? p.N : p.M;
-    if ((g.pc0 & 3) || p.K % BK || m.so != 1 || m.sk <= 1) return false;
+    if ((g.pc0 & 3) || p.K % (128 / (int64_t)sizeof(T)) || m.so != 1 || m.sk <= 1) return false;
     // 32-bit byte offsets over the operand's K stored rows
     return ((p.K - 1) * m.sk + mnO) * (int64_t)sizeof(T) < ((int64_t)1 << 32);
 }
@@ -2208,7 +2238,7 @@ static hipError_t launch_gemm(const GemmProblem &p, hipStream_t s) {
         if (p.ykind == GEN_OO) { RBH_STREAM_L(GEN_OO, false); }
 #undef RBH_STREAM_L
     }
-    if constexpr (sizeof(T) == 8) {
+    {
         if (kernel == PLAN_STREAM_T) {
 #define RBH_STREAM_T(GK, GX)                                                                   \
     return unif ? launch_stream<T, GK, rb::UNIFORM, GX, 5>(p, s) : launch_stream<T, GK, rb::GAUSSIAN, GX, 5>(p, s)

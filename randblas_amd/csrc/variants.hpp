@@ -28,7 +28,9 @@
 // forms (one-triangle and transposed operands: their part-blocks are four 8-B loads). With 1, C5p took
 // 5.50-5.55 ms against 4.26-4.32 (tools/time_tri.py, same box): blocks inside the triangle as four
 // 8-B loads a lane touch 16 cache lines per instruction (64 a part-block, twice full storage's) and
-// run at half speed (all-inside ablation 7.1 ms; all-mirrored 3.87-3.95 ms = 89-90 % of the f64 peak)
+// run at half speed (all-inside ablation 7.1 ms; all-mirrored 3.87-3.95 ms = 89-90 % of the f64 peak);
+// 16-B loads for them with per-class counted waits (uniform branches) made both forms slower (64 x 512
+// 4.89 ms, 32 x 1024 4.63 ms)
 #ifndef RBH_TRI_WIDE
 #define RBH_TRI_WIDE 0
 #endif

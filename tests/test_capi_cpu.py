@@ -147,10 +147,13 @@ def test_plan_options_fix_the_split():
     assert _plan(128, 4096, 4096, opts=rb.Options(splitk=3)) == rb.Plan("stream", 3, 16, 48)
     assert _plan(1024, 16384, 16384, opts=rb.Options(splitk=2)).splitk == 2
     # RowMajor A with lda = n is contiguous along the output columns, not along the contracted
-    # index: f64 streams it down its stored rows (stream_t, the full-grid 32 x 1024 tiles); f32 and
-    # an operand past 32-bit byte offsets take the generic kernel (scalar loads along the outer index)
+    # index: the streamed kernel reads it down its stored rows (stream_t, the full-storage call's
+    # tiles); K off the step depth or an operand past 32-bit byte offsets take the generic kernel
+    # (scalar loads along the outer index)
     assert _plan(1024, 16384, 16384, layout="R") == rb.Plan("stream_t", 1, 512, 512)
-    assert _plan(1024, 16384, 16384, layout="R", dtype="f32").kernel == "generic"
+    p32 = _plan(1024, 16384, 16384, dtype="f32")
+    assert _plan(1024, 16384, 16384, layout="R", dtype="f32") == rb.Plan("stream_t", p32.splitk, p32.tiles, p32.workgroups)
+    assert _plan(256, 4096, 4004, layout="R", dtype="f32").kernel == "generic"
     assert _plan(1024, 32768, 32768, layout="R").kernel == "generic"
     # the materialised window: the 64 x 512 kernels that load it (the same sums)
     assert _plan(1024, 16384, 16384, opts=rb.Options(materialise=True)).kernel == "wide"

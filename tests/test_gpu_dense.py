@@ -475,32 +475,35 @@ STREAM_T_SHAPES = {"ragged": (100, 2100, 256), "split": (64, 1100, 4096), "full"
                    "bg32split": (122, 3000, 4096)}
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("side", ["L", "R"])
 @pytest.mark.parametrize("fam,maj", [("G", "L"), ("G", "S"), ("U", "L")])
 @pytest.mark.parametrize("shape", sorted(STREAM_T_SHAPES))
-def test_transposed_operand_stream_bitwise(cuda, side, fam, maj, shape):
+def test_transposed_operand_stream_bitwise(cuda, dtype, side, fam, maj, shape):
     d, no, K = STREAM_T_SHAPES[shape]   # output rows (generated), outer memory index, contracted index
     rng = np.random.default_rng(11)
     Am = rng.standard_normal((K, no)) if side == "L" else rng.standard_normal((no, K))   # logical op(A)
+    Am = Am.astype(dtype)
+    tag, tdt, ut = ("f64", torch.float64, np.uint64) if dtype == np.float64 else ("f32", torch.float32, np.uint32)
     out, plans = [], []
     for opA in ("N", "T"):
         if side == "L":   # B (d x no, RowMajor) = S (d x K) A (K x no)
             S = rb.DenseSkOp(rb.DenseDist(d + 6, K + 32, fam, maj), rb.RNGState(3))
             A = dev(Am.reshape(-1) if opA == "N" else Am.T.reshape(-1), cuda)   # RowMajor A or A^T
             lda = no if opA == "N" else K
-            B = torch.full((d * no,), 7.0, dtype=torch.float64, device=cuda)
-            plans.append(rb.plan_left("R", "N", opA, d, no, K, S, A, lda, no, ro_s=4, co_s=8))
-            rb.sketch_general_left("R", "N", opA, d, no, K, 1.5, S, A, lda, -0.5, B, no, ro_s=4, co_s=8)
+            B = torch.full((d * no,), 7.0, dtype=tdt, device=cuda)
+            plans.append(rb.plan_left("R", "N", opA, d, no, K, S, A, lda, no, ro_s=4, co_s=8, dtype=tag))
+            rb.sketch_general_left("R", "N", opA, d, no, K, dtype(1.5), S, A, lda, dtype(-0.5), B, no, ro_s=4, co_s=8)
         else:             # B (no x d, ColMajor) = A (no x K) S (K x d)
             S = rb.DenseSkOp(rb.DenseDist(K + 32, d + 6, fam, maj), rb.RNGState(3))
             A = dev(Am.T.reshape(-1) if opA == "N" else Am.reshape(-1), cuda)   # ColMajor A or A^T
             lda = no if opA == "N" else K
-            B = torch.full((no * d,), 7.0, dtype=torch.float64, device=cuda)
-            plans.append(rb.plan_right("C", opA, "N", no, d, K, A, lda, S, no, ro_s=8, co_s=4))
-            rb.sketch_general_right("C", opA, "N", no, d, K, 1.5, A, lda, S, -0.5, B, no, ro_s=8, co_s=4)
+            B = torch.full((no * d,), 7.0, dtype=tdt, device=cuda)
+            plans.append(rb.plan_right("C", opA, "N", no, d, K, A, lda, S, no, ro_s=8, co_s=4, dtype=tag))
+            rb.sketch_general_right("C", opA, "N", no, d, K, dtype(1.5), A, lda, S, dtype(-0.5), B, no, ro_s=8, co_s=4)
         out.append(host(B))
     assert plans[0].kernel == "stream_t" and plans[1].kernel == "stream", plans
     assert (plans[0].splitk, plans[0].tiles) == (plans[1].splitk, plans[1].tiles), plans
-    if shape == "full":
+    if shape == "full" and dtype == np.float64:
         assert plans[0].tiles == (d // 32) * (no // 1024) and plans[0].splitk == 1, plans
-    assert np.array_equal(out[0].view(np.uint64), out[1].view(np.uint64)), f"{np.sum(out[0] != out[1])} differ"
+    assert np.array_equal(out[0].view(ut), out[1].view(ut)), f"{np.sum(out[0] != out[1])} differ"
