@@ -1324,6 +1324,21 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     }
     typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
     u32x4_t mrs4 = {mb_lo, mb_hi & 0xffffu, (uint32_t)mrange, 0x00020000u};   // mrsrc as SGPRs for the asm loads
+    // TRI 5: the resource is re-based at the first stored row of every round (two 64-bit SALU adds a
+    // round), so an operand past 4 GiB streams with 32-bit offsets; its range is what lies past that row
+    uint32_t kb_row = 0;   // the stored row the resource starts at
+    auto rebase = [&](int64_t kt) {
+        if constexpr (TRI == 5) {
+            kb_row = (uint32_t)kt * (uint32_t)KS;
+            const uint64_t off = (uint64_t)kb_row * (uint64_t)mop.sk * sizeof(T);
+            const uint64_t total = ((uint64_t)(p.K - 1) * (uint64_t)mop.sk + (uint64_t)mnO) * sizeof(T);
+            const uint64_t base = (((uint64_t)mb_hi << 32) | mb_lo) + off;
+            const uint64_t rem = total > off ? total - off : 0;
+            mrs4[0] = (uint32_t)base;
+            mrs4[1] = (uint32_t)(base >> 32) & 0xffffu;
+            mrs4[2] = rem > 0xffffffffull ? 0xffffffffu : (uint32_t)rem;
+        }
+    };
     // Diagonal blocks (one-triangle operand): the 16 x 16 blocks on A's diagonal, expanded to both
     // triangles in a small workspace before the launch (tri_diag_kernel; 2 KiB per block, row o's 16
     // values contiguous), loaded like a block inside the triangle: lane (g, r) part p at 128 r + 32 g +
@@ -1359,7 +1374,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
         if constexpr (TRI != 0) {
             const uint32_t K0 = (uint32_t)kt * KS;
             t.cd = ((int32_t)K0 - wm0_32) >> 4;
-            t.so_mir = rowbase(K0) * (uint32_t)sizeof(T);
+            t.so_mir = (TRI == 5 ? (K0 - kb_row) * tso : rowbase(K0)) * (uint32_t)sizeof(T);
             t.so_dia = K0 * 16u * (uint32_t)sizeof(T);
             t.so_in = (uint32_t)kt * 128u;
 #pragma unroll
@@ -1522,6 +1537,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     // prologue: round 0's generated tiles, the first PF blocks of step kt0
 #pragma unroll
     for (int u = 0; u < WCALLS; ++u) draw(u, kt0, 0, kt1);
+    rebase(kt0);
     if (kt0 < kt1) {
         const TriStep t0 = tri_step(kt0);
 #pragma unroll
@@ -1533,6 +1549,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     for (int64_t rd = 0; rd < nrounds; ++rd) {
         const int half = (int)(rd & 1);
         const int64_t kr0 = kt0 + rd * R;
+        if (rd > 0) rebase(kr0);   // (the loads already issued keep the resource they were issued with)
 #pragma unroll
         for (int ts = 0; ts < R; ++ts) {
             const int64_t kt = kr0 + ts;
@@ -2157,8 +2174,9 @@ static bool stream_t_ok(const GemmProblem &p) {
     const MemOperand &m = gx ? p.ym : p.xm;
     const int64_t mnO = gx ? p.N : p.M;
     if ((g.pc0 & 3) || p.K % (128 / (int64_t)sizeof(T)) || m.so != 1 || m.sk <= 1) return false;
-    // 32-bit byte offsets over the operand's K stored rows
-    return ((p.K - 1) * m.sk + mnO) * (int64_t)sizeof(T) < ((int64_t)1 << 32);
+    // 32-bit byte offsets from the round's first stored row (the kernel re-bases its resource every
+    // round of 4 steps; a prefetch reaches at most 6 steps past it)
+    return ((int64_t)128 * m.sk + mnO) * (int64_t)sizeof(T) < ((int64_t)1 << 32);
 }
 
 // Which kernel launch_gemm runs for p, with its tiles and split (the same tests, in the same order).

@@ -148,13 +148,13 @@ def test_plan_options_fix_the_split():
     assert _plan(1024, 16384, 16384, opts=rb.Options(splitk=2)).splitk == 2
     # RowMajor A with lda = n is contiguous along the output columns, not along the contracted
     # index: the streamed kernel reads it down its stored rows (stream_t, the full-storage call's
-    # tiles); K off the step depth or an operand past 32-bit byte offsets take the generic kernel
-    # (scalar loads along the outer index)
+    # tiles, past 4 GiB too: the kernel re-bases its buffer resource every round); K off the step
+    # depth takes the generic kernel (scalar loads along the outer index)
     assert _plan(1024, 16384, 16384, layout="R") == rb.Plan("stream_t", 1, 512, 512)
     p32 = _plan(1024, 16384, 16384, dtype="f32")
     assert _plan(1024, 16384, 16384, layout="R", dtype="f32") == rb.Plan("stream_t", p32.splitk, p32.tiles, p32.workgroups)
     assert _plan(256, 4096, 4004, layout="R", dtype="f32").kernel == "generic"
-    assert _plan(1024, 32768, 32768, layout="R").kernel == "generic"
+    assert _plan(1024, 32768, 32768, layout="R").kernel == "stream_t"
     # the materialised window: the 64 x 512 kernels that load it (the same sums)
     assert _plan(1024, 16384, 16384, opts=rb.Options(materialise=True)).kernel == "wide"
     # (the f32 materialised kernel takes the streamed kernel's split: the same bits)

@@ -507,3 +507,27 @@ def test_transposed_operand_stream_bitwise(cuda, dtype, side, fam, maj, shape):
     if shape == "full" and dtype == np.float64:
         assert plans[0].tiles == (d // 32) * (no // 1024) and plans[0].splitk == 1, plans
     assert np.array_equal(out[0].view(ut), out[1].view(ut)), f"{np.sum(out[0] != out[1])} differ"
+
+
+# The transposed operand past 4 GiB: the kernel re-bases its buffer resource at the first stored row of
+# every round, so offsets stay 32-bit. RowMajor A of 32768 x 32768 f32 (4 GiB) and 24576 x 24576 f64
+# (4.5 GiB), made on the device; bitwise the sketch of its transpose read along k.
+@pytest.mark.parametrize("dtype,nn", [(np.float32, 32768), (np.float64, 24576)])
+def test_transposed_operand_past_4gib(cuda, dtype, nn):
+    d = 64
+    tdt = torch.float32 if dtype == np.float32 else torch.float64
+    tag, ut = ("f32", np.uint32) if dtype == np.float32 else ("f64", np.uint64)
+    g = torch.Generator(device=cuda).manual_seed(5)
+    A = torch.randn(nn, nn, dtype=tdt, device=cuda, generator=g)   # RowMajor K x no (K = no = nn)
+    S = rb.DenseSkOp(rb.DenseDist(d, nn), rb.RNGState(7))
+    outs, plans = [], []
+    for opA in ("N", "T"):
+        X = A if opA == "N" else A.t().contiguous()
+        B = torch.zeros(d * nn, dtype=tdt, device=cuda)
+        plans.append(rb.plan_left("R", "N", opA, d, nn, nn, S, X, nn, nn, dtype=tag))
+        rb.sketch_general_left("R", "N", opA, d, nn, nn, dtype(1.0), S, X, nn, dtype(0.0), B, nn)
+        outs.append(host(B))
+        del X
+    assert plans[0].kernel == "stream_t" and plans[1].kernel == "stream", plans
+    assert np.array_equal(outs[0].view(ut), outs[1].view(ut)), f"{np.sum(outs[0] != outs[1])} differ"
+    assert np.isfinite(outs[0]).all() and np.abs(outs[0]).max() > 0
