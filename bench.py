@@ -1,9 +1,10 @@
 """bench.py -- RandBLAS sketch-apply on MI355X: sketched entries/s and fraction of roofline.
 
-Workload (BASELINE.json configs[1], the metric's single-GPU config): Gaussian skge, fp64,
+Headline workload (north_star's config, where its >= 60 % target is quoted): Gaussian skge, fp64,
 B (d x n) = S (d x m) * A (m x n) with S ~ DenseDist(d, m) (key 0, MajorAxis::Long) regenerated
 inside the fused MFMA GEMM, A ~ DenseDist(m, n) Gaussian key 99 ColMajor (generated on the device,
-resident in HBM before timing), d = 1024, m = n = 16384, alpha = 1, beta = 0.
+resident in HBM before timing), d = 2048, m = n = 16384, alpha = 1, beta = 0. BASELINE configs[1]
+(d = 1024) is the first sub-record, c2.
 
 A "step" is one sketch_general call over the whole A. With N > 1 ranks (torchrun, RCCL) the job is
 sharded by output rows (ro_s, the reference's reproducible-submatrix property) and an RCCL
@@ -25,11 +26,13 @@ GEMM kernel's algorithmic flops (2*d*m*n per launch) / its average launch time m
 events on the launch stream; cpu_baseline = the oracle's OpenMP fill + host BLAS dgemm (the
 reference's algorithm, oracle/) on a bounded column sample, rank 0 only.
 
-Without --config the line also carries "configs": every other BASELINE workload (NS, C3 sampled and
-pre-filled, C4 per GPU, C5, C5p, C1), each timed in this same process with the same steps and
-warm-up, after the headline, with its own ms_per_step, kernel_ms, roofline (traffic + its source),
-plan and a shorter CPU baseline. `--config X` times X alone as the line's top level. Sharded runs
-also report single_call_ms: one step timed alone, its whole all-gather included.
+Without --config the line also carries "configs": every other BASELINE workload (C2, C3 sampled and
+pre-filled, C4 per GPU, C4 whole on one GPU, C5, C5p, C1), each timed in this same process with the
+same steps and warm-up, after the headline. A sub-record holds numbers only (value, ms_per_step,
+kernel_ms, roofline frac / achieved / traffic + its source, plan, cpu_baseline value / cores /
+seconds); what each config is and how it was measured is said once, in the line's "legend".
+`--config X` times X alone as the line's top level. Sharded runs also report single_call_ms: one
+step timed alone, its whole all-gather included.
 """
 from __future__ import annotations
 
@@ -55,7 +58,7 @@ HBM_PEAK = 8.0e12
 
 # --split-d (fixed problem, strong scaling): the TOTAL operator rows, split over the ranks. c4's
 # weak-scaled d = 256 per GPU is configs[3]'s d = 2048 over 8 GPUs; the others are their own total.
-D_TOTAL = {"c1": 128, "c2": 1024, "ns": 2048, "c4": 2048, "c5": 512, "c5p": 512}
+D_TOTAL = {"c1": 128, "c2": 1024, "ns": 2048, "c4": 2048, "c4full": 2048, "c5": 512, "c5p": 512}
 
 CONFIGS = {
     # name: (kind, dtype, d, m, n, vec_nnz)
@@ -64,6 +67,7 @@ CONFIGS = {
     "ns": ("dense", "f64", 2048, 16384, 16384, 0),
     "c3": ("saso", "f64", 1024, 16384, 16384, 8),
     "c4": ("dense", "f32", 256, 32768, 32768, 0),    # per GPU: d = 2048 at N = 8 (configs[3])
+    "c4full": ("dense", "f32", 2048, 32768, 32768, 0),   # configs[3]'s whole problem on one GPU (N = 1 of its strong scaling)
     "c5": ("sksy", "f64", 512, 16384, 16384, 0),
     "c5p": ("sksyp", "f64", 512, 16384, 16384, 0),   # configs[4] as worded: packed-symmetric A
 }
@@ -228,13 +232,72 @@ WORKLOADS = {"c1": "Gaussian skge fp64 d=128 A 4096^2 (BASELINE configs[0], the 
              "ns": "Gaussian skge fp64 north-star",
              "c3": "SASO SparseSkOp vec_nnz=8 fp64 (configs[2])",
              "c4": "Gaussian skge fp32 (configs[3])",
+             "c4full": "Gaussian skge fp32, configs[3]'s whole d=2048 on one GPU",
              "c5": "sksy fp64, sketch_symmetric with sym_check_tol=0 (configs[4])",
              "c5p": "sksy fp64 on packed-symmetric A (configs[4] as worded)"}
 
-# The configs a default run times after the headline (c2), each in this process with the same steps
-# and warm-up: (record name, config, SASO operator filled once before timing)
-SUB_CONFIGS = [("ns", "ns", False), ("c3", "c3", False), ("c3_prefilled", "c3", True), ("c4", "c4", False),
-               ("c5", "c5", False), ("c5p", "c5p", False), ("c1", "c1", False)]
+# The configs a default run times after the headline (ns), each in this process with the same steps and
+# warm-up: (record name, config, SASO operator filled once before timing)
+SUB_CONFIGS = [("c2", "c2", False), ("c3", "c3", False), ("c3_prefilled", "c3", True), ("c4", "c4", False),
+               ("c4_full", "c4full", False), ("c5", "c5", False), ("c5p", "c5p", False), ("c1", "c1", False)]
+
+# One description per record name, printed once in the line's "legend" (the sub-records carry numbers only)
+LEGEND = {
+    "ns": "headline: Gaussian skge f64 d=2048 m=n=16384 ColMajor (north_star's config)",
+    "c2": "Gaussian skge f64 d=1024 m=n=16384 (BASELINE configs[1])",
+    "c3": "SASO vec_nnz=8 f64 d=1024 m=n=16384, operator sampled in every call (configs[2])",
+    "c3_prefilled": "c3 with the operator filled once, applied from its arrays (fill-once / apply-many)",
+    "c4": "Gaussian skge f32 d=256 m=n=32768: one GPU's row shard of configs[3] at N=8",
+    "c4_full": "Gaussian skge f32 d=2048 m=n=32768: configs[3]'s whole problem on one GPU",
+    "c5": "sketch_symmetric f64 d=512 n=16384, full storage, sym_check_tol=0 timed in the step (configs[4])",
+    "c5p": "sketch_symmetric_triangle f64 d=512 n=16384 on packed upper A (configs[4] as worded)",
+    "c1": "Gaussian skge f64 d=128 m=n=4096 (configs[0], the reference's CPU case)",
+    "fields": "value entries/s; kernel_ms: dominant kernel, HIP events; frac: algorithmic 2dmn flops (SASO: "
+              "(m+d)n*8 B) / kernel_ms / peak (f64 78.6 TF, f32 157.3 TF, HBM 8 TB/s); achieved in TFLOP/s (SASO "
+              "GB/s); traffic: PMC HBM B per launch (traffic_source)",
+    "data": "synthetic A, Gaussian key 99, generated on device; dense S drawn in the GEMM, never stored",
+    "cpu_baseline": "oracle port (OpenMP fill + OpenBLAS gemm; SASO: COO scatter) on a column sample",
+}
+
+
+def _r(x, sig=5):
+    """x to `sig` significant digits (sub-records: numbers only, short)."""
+    return None if x is None else float(f"{x:.{sig}g}")
+
+
+def compact(rec):
+    """A sub-record's numbers (the prose lives in LEGEND): what the driver's stored tail must hold."""
+    if "error" in rec:
+        return rec
+    rf = rec["roofline"]
+    src = rf.get("traffic_source")
+    out = {"value": _r(rec["value"]), "ms_per_step": _r(rec["ms_per_step"]), "kernel_ms": _r(rec["kernel_ms"]),
+           "dtype": rec["dtype"],
+           "roofline": {"frac": _r(rf["frac"], 4), "achieved": _r(rf["achieved"], 4), "traffic": rf["traffic"],
+                        "traffic_source": src.split(":")[0] if src else None},
+           "plan": rec["plan"]}
+    for k in ("compute_ms_per_step", "exposed_exchange_ms_per_step", "single_call_ms"):
+        if rec.get(k) is not None:
+            out[k] = _r(rec[k])
+    cb = rec.get("cpu_baseline")
+    out["cpu_baseline"] = None if cb is None else {"value": _r(cb["value"]), "cores": cb["cores"],
+                                                   "seconds": _r(cb["seconds"], 3)}
+    return out
+
+
+def format_line(head, sub, args, world, headline):
+    """The one JSON line rank 0 prints: the headline's full record, the sub-records' numbers, the legend."""
+    line = {"metric": "sketched-entries/sec (d*n/s) + achieved-%-of-fp64-MFMA-peak, skge d x m * m x n",
+            "value": head.pop("value"), "unit": head.pop("unit"), "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": head.pop("ms_per_step"), "higher_is_better": True,
+            "scaling": head.pop("scaling"), "vs_baseline": None}
+    line.update(head)
+    if sub:
+        # every other BASELINE config, timed in this same process with the same steps and warm-up
+        line["configs"] = {name: compact(rec) for name, rec in sub.items()}
+        line["legend"] = {k: v for k, v in LEGEND.items()
+                          if k in sub or k == headline or k in ("fields", "data", "cpu_baseline")}
+    return line
 
 
 def run_config(args, config, prefilled, world, rank, dev, use_dist):
@@ -449,7 +512,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
-                    help="time this config alone (default: the headline c2, then every other BASELINE config "
+                    help="time this config alone (default: the headline ns, then every other BASELINE config "
                          "as sub-records of the same line)")
     ap.add_argument("--no-configs", action="store_true", help="the headline config only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -472,7 +535,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="CPU work per baseline sample of the headline config (sub-configs: a third of it)")
     args = ap.parse_args()
-    headline = args.config or "c2"
+    headline = args.config or "ns"
     subs = [] if (args.config or args.no_configs) else SUB_CONFIGS
     if args.split_d:   # strong scaling applies to the dense configs only
         subs = [sc for sc in subs if CONFIGS[sc[1]][0] != "saso"]
@@ -523,15 +586,7 @@ def main():
                 log(f"cpu_baseline failed: {e!r}")
 
     if rank == 0:
-        line = {"metric": "sketched-entries/sec (d*n/s) + achieved-%-of-fp64-MFMA-peak, skge d x m * m x n",
-                "value": head.pop("value"), "unit": head.pop("unit"), "n_gpus": world, "steps": args.steps,
-                "warmup": args.warmup, "ms_per_step": head.pop("ms_per_step"), "higher_is_better": True,
-                "scaling": head.pop("scaling"), "vs_baseline": None}
-        line.update(head)
-        if sub:
-            # every other BASELINE config, timed in this same process with the same steps and warm-up
-            line["configs"] = sub
-        print(json.dumps(line), flush=True)
+        print(json.dumps(format_line(head, sub, args, world, headline)), flush=True)
     if use_dist:
         dist.destroy_process_group()
 
