@@ -1844,6 +1844,13 @@ static hipError_t materialise(const GemmProblem &p, void **buf, hipStream_t s) {
     return e;
 }
 
+// The streamed kernel's launcher. Its instantiations (192 -> 160 kernels) are compiled in five
+// translation units of their own, this file built again with RBH_STREAM_PART = 0 .. 4 (Makefile):
+// one per (T, operand form), so the build runs them in parallel (the single file took 6 minutes).
+// This translation unit only calls them.
+template <typename T, int GK, int FAMILY, bool GX, int TRI = 0>
+hipError_t launch_stream(const GemmProblem &p, hipStream_t s);
+
 struct StreamGeom {
     int bg;      // generated rows per tile
     int mw;      // memory rows per wave (the tile's memory rows: 8 mw)
@@ -2036,13 +2043,22 @@ __global__ __launch_bounds__(256) void tri_diag_kernel(const double *A, int64_t 
 // part-blocks loaded ahead of their use (a register ring of PF + 1; PF + 1 divides 8)
 template <typename T> constexpr int stream_pf() { return sizeof(T) == 8 ? RBH_PF64 : RBH_PF32; }
 
-template <typename T, int GK, int FAMILY, bool GX, int TRI = 0>
-static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
+#if defined(RBH_STREAM_PART)
+template <typename T, int GK, int FAMILY, bool GX, int TRI>
+hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
     const int64_t gnO = GX ? p.M : p.N, mnO = GX ? p.N : p.M;
     StreamGeom gm = stream_geom<T>(p);
-    // one-triangle operands: the full-storage call's tiles (RBH_TRI_WIDE), else 64 x 512 (the split is
-    // the same either way, so the sums are full storage's bits)
-    if (TRI && TRI != 5 && !RBH_TRI_WIDE) gm = StreamGeom{64, 64, gm.split};
+    // one-triangle operands (TRI 1-4): 64 x 512 tiles always, with the full-storage call's split (so
+    // the sums are full storage's bits). Round 5 measured them on the full-storage call's 32 x 1024 /
+    // 32 x 512 tiles as well (C5p 5.50-5.55 ms against 4.26-4.32: in-triangle blocks as four 8-B loads a
+    // lane touch 16 cache lines per instruction); that build also failed the bitwise suite
+    // (test_sksy_tri_ragged_full_grid, 844,800 values), and its kernels spill 24-64 B a lane
+    // (-Rpass-analysis=kernel-resource-usage): with the ring loaded by inline asm the compiler takes a
+    // register as written when the load issues, so a spill copies it before the data lands. The
+    // switch (RBH_TRI_WIDE) is gone; tools/check_spills.py fails the build if any streamed kernel with
+    // a one-triangle or transposed operand spills.
+    constexpr bool TRI64 = TRI != 0 && TRI != 5;
+    if (TRI64) gm = StreamGeom{64, 64, gm.split};
     const int64_t nb = ((gnO + gm.bg - 1) / gm.bg) * ((mnO + 8 * gm.mw - 1) / (8 * gm.mw));
     if (nb <= 0) return hipSuccess;
     const int split = gm.split;
@@ -2073,7 +2089,10 @@ static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
     const dim3 grid((unsigned)(nb * split));
     constexpr int PF = (TRI && TRI != 5) ? RBH_PF_TRI : stream_pf<T>();
     constexpr int PF32 = TRI ? RBH_PF_TRI32 : stream_pf<T>();   // 32-row tiles
-    if constexpr (sizeof(T) == 8) {   // 32 x 1024 or 64 x 512 tiles (64 x 1024 would take 256 accumulator registers)
+    if constexpr (TRI64) {   // 64 x 512 only
+        if (split > 1) hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, true, PF, 64, 64, TRI>), grid, dim3(512), 0, s, q);
+        else hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, PF, 64, 64, TRI>), grid, dim3(512), 0, s, q);
+    } else if constexpr (sizeof(T) == 8) {   // 32 x 1024 or 64 x 512 tiles (64 x 1024 would take 256 accumulator registers)
         if (gm.mw == 128) {   // full unsplit grids: 32 x 1024 tiles (stream_geom)
             hipLaunchKernelGGL((skge_stream_kernel<T, GK, FAMILY, GX, false, PF32, 32, 128, TRI>), grid, dim3(512), 0, s, q);
         } else if (gm.bg == 32) {   // small grids: 32 x 512 tiles (stream_geom), split K
@@ -2104,6 +2123,9 @@ static hipError_t launch_stream(const GemmProblem &p, hipStream_t s) {
     }
     return e;
 }
+#endif   // RBH_STREAM_PART
+
+#if !defined(RBH_STREAM_PART)
 
 // The one-triangle operand streams by default (RBH_TRI_STREAMED, variants.hpp): skge_stream_kernel
 // with TRI, two 8-B loads per part-block into the register ring (mirrored ones down the stored rows),
@@ -2174,9 +2196,12 @@ static bool stream_t_ok(const GemmProblem &p) {
     const MemOperand &m = gx ? p.ym : p.xm;
     const int64_t mnO = gx ? p.N : p.M;
     if ((g.pc0 & 3) || p.K % (128 / (int64_t)sizeof(T)) || m.so != 1 || m.sk <= 1) return false;
-    // 32-bit byte offsets from the round's first stored row (the kernel re-bases its resource every
-    // round of 4 steps; a prefetch reaches at most 6 steps past it)
-    return ((int64_t)128 * m.sk + mnO) * (int64_t)sizeof(T) < ((int64_t)1 << 32);
+    // 32-bit byte offsets from the round's first stored row. The kernel re-bases its resource at the
+    // first row of every round of R = 4 steps, and the last step of a round prefetches the next step's
+    // part-blocks, so a load reaches stored rows up to 5 KS - 1 past the base (f64 79, f32 159) and
+    // columns up to mnO plus one ragged wave's 16 FB <= 128 elements.
+    const int64_t KS = 128 / (int64_t)sizeof(T);
+    return (5 * KS * m.sk + mnO + 256) * (int64_t)sizeof(T) < ((int64_t)1 << 32);
 }
 
 // Which kernel launch_gemm runs for p, with its tiles and split (the same tests, in the same order).
@@ -2365,5 +2390,34 @@ hipError_t launch_scale_f64(int64_t M, int64_t N, double beta, double *C, int64_
 hipError_t launch_scale_f32(int64_t M, int64_t N, float beta, float *C, int64_t ldc, hipStream_t s) {
     return launch_scale<float>(M, N, beta, C, ldc, s);
 }
+#endif   // !RBH_STREAM_PART
+
+// The streamed launchers this translation unit instantiates (RBH_STREAM_PART): part 0 f64 and part 1
+// f32 memory operands along k, part 2 f64 and part 3 f32 transposed operands (TRI 5), part 4 the f64
+// one-triangle operands (TRI 1-4, counter along k only); every generated form and family of each.
+#define RBH_STREAM_INST(T, GK, TRI)                                                                         \
+    template hipError_t launch_stream<T, GK, rb::GAUSSIAN, true, TRI>(const GemmProblem &, hipStream_t);    \
+    template hipError_t launch_stream<T, GK, rb::UNIFORM, true, TRI>(const GemmProblem &, hipStream_t);     \
+    template hipError_t launch_stream<T, GK, rb::GAUSSIAN, false, TRI>(const GemmProblem &, hipStream_t);   \
+    template hipError_t launch_stream<T, GK, rb::UNIFORM, false, TRI>(const GemmProblem &, hipStream_t);
+#if defined(RBH_STREAM_PART) && RBH_STREAM_PART == 0
+RBH_STREAM_INST(double, GEN_OK, 0)
+RBH_STREAM_INST(double, GEN_OO, 0)
+#elif defined(RBH_STREAM_PART) && RBH_STREAM_PART == 1
+RBH_STREAM_INST(float, GEN_OK, 0)
+RBH_STREAM_INST(float, GEN_OO, 0)
+#elif defined(RBH_STREAM_PART) && RBH_STREAM_PART == 2
+RBH_STREAM_INST(double, GEN_OK, 5)
+RBH_STREAM_INST(double, GEN_OO, 5)
+#elif defined(RBH_STREAM_PART) && RBH_STREAM_PART == 3
+RBH_STREAM_INST(float, GEN_OK, 5)
+RBH_STREAM_INST(float, GEN_OO, 5)
+#elif defined(RBH_STREAM_PART) && RBH_STREAM_PART == 4
+RBH_STREAM_INST(double, GEN_OK, 1)
+RBH_STREAM_INST(double, GEN_OK, 2)
+RBH_STREAM_INST(double, GEN_OK, 3)
+RBH_STREAM_INST(double, GEN_OK, 4)
+#endif
+#undef RBH_STREAM_INST
 
 }  // namespace rbh

@@ -20,25 +20,17 @@
 #ifndef RBH_PF_TRI
 #define RBH_PF_TRI 7
 #endif
-// one-triangle symmetric operands (sketch_symmetric_triangle, packed A): 1 = the streamed kernel
-// (C5p 4.25-4.26 ms against 4.59-4.61 with 0), 0 = skge_wide_kernel's LDS transpose of the mirrored
-// tiles (the materialised-window option always takes it)
-// one-triangle operands on the full-storage call's tile shape (1: 32 x 1024 tiles for full unsplit
-// grids, 32 x 512 for small split grids; 0: always 64 x 512), and the prefetch depth of the 32-row
-// forms (one-triangle and transposed operands: their part-blocks are four 8-B loads). With 1, C5p took
-// 5.50-5.55 ms against 4.26-4.32 (tools/time_tri.py, same box): blocks inside the triangle as four
-// 8-B loads a lane touch 16 cache lines per instruction (64 a part-block, twice full storage's) and
-// run at half speed (all-inside ablation 7.1 ms; all-mirrored 3.87-3.95 ms = 89-90 % of the f64 peak);
-// 16-B loads for them with per-class counted waits (uniform branches) made both forms slower (64 x 512
-// 4.89 ms, 32 x 1024 4.63 ms)
-#ifndef RBH_TRI_WIDE
-#define RBH_TRI_WIDE 0
-#endif
-// (transposed operands, f64 32 x 1024: PF 7 7.74-7.77 ms against 7.80-7.82 with 3 at d = 1024,
-// m = n = 16384, same box, two alternations)
+// prefetch depth of the 32-row transposed-operand forms (TRI 5; their part-blocks are four 8-B
+// loads): f64 32 x 1024 PF 7 7.74-7.77 ms against 7.80-7.82 with 3 at d = 1024, m = n = 16384, same
+// box, two alternations
 #ifndef RBH_PF_TRI32
 #define RBH_PF_TRI32 7
 #endif
+// one-triangle symmetric operands (sketch_symmetric_triangle, packed A): 1 = the streamed kernel
+// on 64 x 512 tiles (C5p 4.25-4.26 ms against 4.59-4.61 with 0), 0 = skge_wide_kernel's LDS transpose
+// of the mirrored tiles (the materialised-window option always takes it). (Round 5's RBH_TRI_WIDE,
+// the one-triangle operand on the full-storage call's 32 x 1024 tiles, measured 5.5 ms against 4.26
+// and spilled ring registers: removed, see launch_stream.)
 #ifndef RBH_TRI_STREAMED
 #define RBH_TRI_STREAMED 1
 #endif

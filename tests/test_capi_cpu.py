@@ -4,6 +4,7 @@ No GPU work is issued here."""
 import ctypes
 import os
 import re
+import sys
 
 import numpy as np
 import pytest
@@ -140,6 +141,50 @@ def test_plan_baseline_configs():
                  opts=rb.Options(splitk=2)) == rb.Plan("stream", 2, 64, 128)
     # K below 2048 never splits (every kernel then adds in the same order)
     assert _plan(128, 4096, 1024).splitk == 1
+
+
+def test_stream_t_offsets_bound_each_dtype():
+    """the transposed-operand stream re-bases its buffer resource once per round of 4 steps
+    and prefetches into the next step, so its 32-bit offsets reach 5 steps of stored rows past the
+    base: 80 rows for f64 (KS = 16), 160 for f32 (KS = 32). The plan takes stream_t exactly while
+    (5 KS lda + n + 256) * sizeof(T) < 2^32 (f32: lda < 6,710,884 at n = 128; the old 128-row bound
+    let f32 strides up to 8.4 M through, whose offsets wrapped) and the generic kernel past it."""
+    S = rb.DenseSkOp(rb.DenseDist(64, 1024), rb.RNGState(0))
+    def kern(dtype, lda):
+        return rb.plan_left("R", "N", "N", 64, 128, 1024, S, 256, lda, 128, dtype=dtype).kernel
+    for dtype, esz in (("f32", 4), ("f64", 8)):
+        ks = 128 // esz
+        lim = ((1 << 32) // esz - 128 - 256 + 5 * ks - 1) // (5 * ks)   # first lda whose reach overflows
+        assert kern(dtype, lim - 1000) == "stream_t", dtype
+        assert kern(dtype, lim + 1000) != "stream_t", dtype
+    # f64 reaches 80 rows, not 128: strides the old bound refused now stream (4.19 M < lda < 6.7 M)
+    assert kern("f64", 5_000_000) == "stream_t"
+
+
+def test_spill_guard_reads_the_compiler_remarks(tmp_path):
+    """tools/check_spills.py (run by the Makefile on every skge object) fails the build for a streamed
+    kernel with an asm-loaded ring (TRI 1-5) that spills VGPRs, and passes TRI 0 spills (compiler-visible
+    loads) and SGPR spills (they go to VGPR lanes)."""
+    import subprocess
+    def remarks(name, scratch, vspill, sspill=0):
+        r = f"skge_dense.hip:1211:1: remark: Function Name: {name} [-Rpass-analysis=kernel-resource-usage]\n"
+        for k, v in (("VGPRs", 256), ("ScratchSize [bytes/lane]", scratch), ("SGPRs Spill", sspill),
+                     ("VGPRs Spill", vspill)):
+            r += f"skge_dense.hip:1211:1: remark:     {k}: {v} [-Rpass-analysis=kernel-resource-usage]\n"
+        return r + " 1211 | __global__ void f() {\n      | ^\n"
+    tri3 = "_ZN3rbh18skge_stream_kernelIdLi1ELi1ELb0ELb0ELi7ELi32ELi128ELi3EEEvNS_11GemmProblemE"
+    tri0 = "_ZN3rbh18skge_stream_kernelIdLi1ELi1ELb0ELb0ELi7ELi32ELi128ELi0EEEvNS_11GemmProblemE"
+    tool = os.path.join(ROOT, "tools", "check_spills.py")
+    for text, rc in ((remarks(tri3, 56, 13), 1), (remarks(tri3, 0, 0, 7), 0), (remarks(tri0, 40, 9), 0)):
+        f = tmp_path / "r.txt"
+        f.write_text(text)
+        r = subprocess.run([sys.executable, tool, str(f)], capture_output=True, text=True)
+        assert r.returncode == rc, (text, r.stderr)
+        assert "1211 |" not in r.stderr
+    # the product build's own remarks: every object passes
+    import glob
+    for f in glob.glob(os.path.join(ROOT, "randblas_amd", "_obj", "*.remarks")):
+        assert subprocess.run([sys.executable, tool, f], capture_output=True).returncode == 0, f
 
 
 def test_plan_options_fix_the_split():
