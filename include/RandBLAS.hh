@@ -386,8 +386,11 @@ struct SparseSkOp {
     const bool own_memory = true;
     bool known_filled = false;
     // Extension: the arrays hold this header's fill_sparse(S) output. For device arrays the apply
-    // then tells the library so (rbh_options.sparse_filled) and does not wait for its device check;
-    // clear it after writing to the arrays yourself (a false claim makes the sketch NaN).
+    // then tells the library so (rbh_options.sparse_filled) and does not wait for its device check.
+    // Writing to the arrays without clearing it (e.g. scaling vals by isometry_scale_factor) stays
+    // correct: the check runs on the device and, when it fails, a fallback gated on its flag computes
+    // the sketch (rbh_sparse_last_path() == 5 once the stream has run); clearing it after a write
+    // saves the fast apply's discarded work.
     bool filled_by_library = false;
     sint_t *rows = nullptr;
     sint_t *cols = nullptr;

@@ -157,9 +157,12 @@ int rbh_rskge3_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_
  *                  a device check: with 0 (default) the call waits for that check on the host (and
  *                  falls back to the sorted apply when it fails; on a stream being captured into a
  *                  graph, where it cannot wait, it takes the sorted apply directly); with 1 it does
- *                  not wait, and a failed check makes the sketch NaN. The claim is honoured only
- *                  with |alpha| = 1 (fill_sparse's values are +-1); with any other alpha the call
- *                  waits as with 0. */
+ *                  not wait: when the check fails (the claim was false: values rescaled or
+ *                  rewritten, repeated entries) the fast apply writes nothing and a fallback gated
+ *                  on the check's device flag computes B from the arrays, bitwise the reference's
+ *                  loop; rbh_sparse_last_path() then returns 5. The claim is honoured only with
+ *                  |alpha| = 1 (fill_sparse's values are +-1); with any other alpha the call waits
+ *                  as with 0. */
 typedef struct rbh_options {
     int32_t splitk;
     int32_t materialise;
@@ -231,7 +234,9 @@ int rbh_rskges_ex_f32(char layout, char opA, char opS, int64_t m, int64_t d, int
 /* Which apply the calling thread's last sparse sketch (or spmm / sketch_sparse) ran: 0 none (empty
  * output), 1 the LDS-DMA kernel on a sort-free CSR (operators whose values are +-1 after alpha,
  * without repeated entries), 2 the row gather (very sparse operators), 3 the sorted CSR with the
- * uniform-value kernel, 4 the sorted CSR with the general kernel. */
+ * uniform-value kernel, 4 the sorted CSR with the general kernel, 5 the device-gated fallback of a
+ * false sparse_filled claim (rbh_options). A call with sparse_filled = 1 decides between 1 and 5 on
+ * the device: until its stream has run it, this returns 6 (pending); synchronise the stream first. */
 int rbh_sparse_last_path(void);
 
 /* ---- sketch_general, sparse operator ----------------------------------------------------- */

@@ -130,12 +130,18 @@ lib.rbh_release_workspaces.argtypes = [c_vp]
 lib.rbh_release_workspaces_ex.argtypes = [c_vp, ctypes.c_int]
 lib.rbh_sketch_symmetric_last_path.restype = ctypes.c_int
 lib.rbh_sparse_last_path.restype = ctypes.c_int
-SPARSE_PATHS = {0: "none", 1: "dma", 2: "gather", 3: "sorted_unit", 4: "sorted"}
+SPARSE_PATHS = {0: "none", 1: "dma", 2: "gather", 3: "sorted_unit", 4: "sorted", 5: "dma_fallback", 6: "pending"}
 
 
 def sparse_last_path() -> str:
-    """Which apply this thread's last sparse sketch ran (rbh_sparse_last_path)."""
-    return SPARSE_PATHS[lib.rbh_sparse_last_path()]
+    """Which apply this thread's last sparse sketch ran (rbh_sparse_last_path). A claimed filled
+    operator (sparse_filled) decides on the device whether the DMA apply or its gated fallback writes
+    B; while the call has not run yet ("pending") this synchronises the device and asks again."""
+    path = SPARSE_PATHS[lib.rbh_sparse_last_path()]
+    if path == "pending":
+        torch.cuda.synchronize()
+        path = SPARSE_PATHS[lib.rbh_sparse_last_path()]
+    return path
 lib.rbh_unpack_shards.argtypes = [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, ctypes.c_int, c_vp]
 for _t, _ct in (("f64", ctypes.c_double), ("f32", ctypes.c_float)):
     getattr(lib, f"rbh_sketch_symmetric_{_t}").argtypes = [c_char, c_char, c_i64, c_i64, _ct, P(DenseDistC),

@@ -25,6 +25,9 @@
 //      The dense operand is read from HBM once per 16-column panel; no atomics, deterministic.
 #include "common.hpp"
 #include "saso.hpp"
+
+#include <atomic>
+#include <mutex>
 #include "variants.hpp"
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -35,7 +38,8 @@ namespace rbh {
 
 // which apply the calling thread's last sparse sketch ran (rbh_sparse_last_path)
 static thread_local int g_sparse_path = SPARSE_PATH_NONE;
-int sparse_last_path() { return g_sparse_path; }
+static int gated_path();
+int sparse_last_path() { return g_sparse_path == SPARSE_PATH_DMA_GATED ? gated_path() : g_sparse_path; }
 
 constexpr int SP_KC = 128;        // contracted indices per chunk (LDS panel depth), section 2
 
@@ -1087,6 +1091,9 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
     const bool jin = j < p.N;
     const T *Y = (const T *)p.Y;
     const T beta = (T)p.beta;
+    // The caller's arrays failed mark_check_kernel's test (a claimed fill_sparse output that was not):
+    // write nothing; the gated fallback after this kernel (fb_bucket_kernel, fb_apply_kernel) computes C.
+    if (bad && *bad) return;
 
     SdAcc acc;
     acc.dmy = (T)0;
@@ -1295,10 +1302,6 @@ __global__ __launch_bounds__(SU_NT) void saso_dma_kernel(const SparseApply p, co
 #undef SD_LOADS
     wait_vm<0>();
     __syncthreads();   // the epilogue reuses the panel memory
-    if (bad && *bad) {   // the caller's arrays failed mark_check_kernel's test: fail loudly
-#pragma unroll
-        for (int r = 0; r < SU_R; ++r) acc.set(r, __builtin_nan(""));
-    }
     su_epilogue<T>(acc, reinterpret_cast<T *>(smem), p, row0, j0, wave, lane, vec_out);
 }
 
@@ -1451,6 +1454,152 @@ __global__ void place_kernel(int64_t nnz, const int64_t *rows, const int64_t *co
         for (int64_t q = pos + 1; q < seg[g + 1]; ++q) rec[q] = pad;
 }
 
+// ------------------------------------------------------------------------------------------
+// 7b. Device-gated fallback of a claimed fill_sparse output (p.arrays_filled = 1, no host wait). A
+//     caller may rescale or rewrite a filled operator's arrays (sparse_skops.hh:167-177: isometry
+//     scaling of S.vals) without telling the library; the claim is then false and the DMA apply
+//     above, whose panel is Y itself, does not apply. It exits at once when mark_check_kernel's flag
+//     is set, and these two kernels, queued behind it, compute the sketch the reference way instead:
+//     they read the same flag and return at once when it is clear (the claim held: two empty
+//     launches), so the call still never waits on the host.
+//   fb_bucket_kernel (one workgroup): per-row counts of the in-window entries, their exclusive scan
+//     (ptr, M + 1), a bucket fill, then each row's bucket sorted by (k, entry index) -- CSR in
+//     ascending k, stable for repeated (row, k) like the library's sorted path.
+//   fb_apply_kernel: lane = output row, one output column per wave and tile: c = (beta == 0 ? 0 :
+//     beta * C(i, j)), then for each of row i's entries in ascending k c = c + (alpha * v) * Y(k, j),
+//     multiply and add rounded separately -- the reference's scalar loop (coo_spmm_impl.hh:138-160,
+//     safe_scal util.hh:51-59), so the result is bitwise the oracle's.
+//   Thread 0 of fb_bucket_kernel also copies the flag to a pinned host word, from which
+//   rbh_sparse_last_path() reports, once the stream has run, which of the two applies wrote C.
+// ------------------------------------------------------------------------------------------
+constexpr int FB_NT = 1024;
+
+__device__ __forceinline__ bool fb_entry(int64_t e, const int64_t *rows, const int64_t *cols, const SparseApply &p,
+                                         int64_t &i, int64_t &k) {
+    const int64_t wr = rows[e] - p.ro, wc = cols[e] - p.co;
+    if (!(wr >= 0 && wr < p.win_r && wc >= 0 && wc < p.win_c)) return false;
+    i = p.transposed ? wc : wr;
+    k = p.transposed ? wr : wc;
+    return true;
+}
+
+__global__ __launch_bounds__(FB_NT) void fb_bucket_kernel(const uint32_t *bad, int64_t nnz, const int64_t *rows,
+                                                          const int64_t *cols, const SparseApply p, int32_t *ptr,
+                                                          int32_t *cur, int32_t *bucket, uint32_t *host_flag) {
+    const int tid = threadIdx.x;
+    const uint32_t f = *bad;
+    if (tid == 0 && host_flag) *(volatile uint32_t *)host_flag = f;
+    if (!f) return;
+    const int64_t M = p.M;
+    for (int64_t r = tid; r <= M; r += FB_NT) ptr[r] = 0;
+    __syncthreads();
+    int64_t i, k;
+    for (int64_t e = tid; e < nnz; e += FB_NT)
+        if (fb_entry(e, rows, cols, p, i, k)) atomicAdd(&ptr[i + 1], 1);
+    __syncthreads();
+    // inclusive scan of ptr[1 .. M] in blocks of FB_NT (ptr[0] = 0): ptr[i] = entries of rows < i
+    __shared__ int32_t wsum[FB_NT / 64];
+    __shared__ int32_t carry;
+    if (tid == 0) carry = 0;
+    __syncthreads();
+    const int lane = tid & 63, wave = tid >> 6;
+    for (int64_t b0 = 1; b0 <= M; b0 += FB_NT) {
+        const int64_t r = b0 + tid;
+        const int32_t c = r <= M ? ptr[r] : 0;
+        int32_t x = c;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[wave] = x;
+        __syncthreads();
+        int32_t base = carry;
+        for (int w = 0; w < wave; ++w) base += wsum[w];
+        if (r <= M) ptr[r] = base + x;
+        __syncthreads();
+        if (tid == FB_NT - 1) carry = base + x;
+        __syncthreads();
+    }
+    for (int64_t r = tid; r < M; r += FB_NT) cur[r] = ptr[r];
+    __syncthreads();
+    for (int64_t e = tid; e < nnz; e += FB_NT)
+        if (fb_entry(e, rows, cols, p, i, k)) bucket[atomicAdd(&cur[i], 1)] = (int32_t)e;
+    __syncthreads();
+    // each row's entries in ascending (k, entry index): insertion sort (rows of a sketching operator
+    // hold tens to hundreds of entries)
+    auto key = [&](int32_t e) -> int64_t { int64_t ii, kk; fb_entry(e, rows, cols, p, ii, kk); return kk; };
+    for (int64_t r = tid; r < M; r += FB_NT) {
+        const int32_t a = ptr[r], b = ptr[r + 1];
+        for (int32_t x = a + 1; x < b; ++x) {
+            const int32_t e = bucket[x];
+            const int64_t ke = key(e);
+            int32_t y = x - 1;
+            while (y >= a) {
+                const int32_t ey = bucket[y];
+                const int64_t ky = key(ey);
+                if (ky < ke || (ky == ke && ey < e)) break;
+                bucket[y + 1] = ey;
+                --y;
+            }
+            bucket[y + 1] = e;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void fb_apply_kernel(const uint32_t *bad, const int64_t *rows, const int64_t *cols,
+                                                       const double *vals, const SparseApply p, const int32_t *ptr,
+                                                       const int32_t *bucket) {
+#pragma clang fp contract(off)   // one rounding per multiply and per add, as the reference's loop
+    if (!*bad) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * 4;
+    const int64_t nrb = (p.M + 63) / 64, tiles = nrb * p.N;
+    const double *Y = (const double *)p.Y;
+    double *C = (double *)p.C;
+    const double alpha = p.alpha, beta = p.beta;
+    for (int64_t t = wave; t < tiles; t += nw) {
+        const int64_t i = (t % nrb) * 64 + lane, j = t / nrb;
+        if (i >= p.M) continue;
+        double *c = C + i * p.crs + j * p.ccs;
+        double acc = beta == 0.0 ? 0.0 : beta * *c;
+        for (int32_t q = ptr[i]; q < ptr[i + 1]; ++q) {
+            const int32_t e = bucket[q];
+            const int64_t k = p.transposed ? rows[e] - p.ro : cols[e] - p.co;
+            const double prod = (alpha * vals[e]) * Y[k * p.ysk + j * p.ysj];
+            acc = acc + prod;
+        }
+        *c = acc;
+    }
+}
+
+// Pinned host words the fallback's flag is copied to (one per call, reused after FB_SLOTS calls), and
+// the calling thread's last one: rbh_sparse_last_path() reads it once the stream has run the call.
+constexpr int FB_SLOTS = 256;
+static uint32_t *g_fb_host = nullptr;
+static std::atomic<int> g_fb_next{0};
+static thread_local int g_fb_slot = -1;
+static uint32_t *fb_host_slot() {
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void *h = nullptr;
+        if (hipHostMalloc(&h, FB_SLOTS * sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess)
+            g_fb_host = (uint32_t *)h;
+        else
+            (void)hipGetLastError();
+    });
+    if (!g_fb_host) { g_fb_slot = -1; return nullptr; }
+    g_fb_slot = g_fb_next.fetch_add(1) % FB_SLOTS;
+    g_fb_host[g_fb_slot] = 0xffffffffu;   // not run yet
+    return g_fb_host + g_fb_slot;
+}
+// a gated call: the DMA apply if the check passed, the fallback if it failed, "pending" before the
+// stream has run fb_bucket_kernel (the flag copy), DMA when no pinned word could be allocated
+static int gated_path() {
+    if (!g_fb_host || g_fb_slot < 0) return SPARSE_PATH_DMA;
+    const uint32_t f = ((volatile uint32_t *)g_fb_host)[g_fb_slot];
+    return f == 0xffffffffu ? SPARSE_PATH_PENDING : (f ? SPARSE_PATH_FALLBACK : SPARSE_PATH_DMA);
+}
+
 // The LDS-DMA apply (section 5) on a sort-free CSR. With gen, the operator is sampled here into
 // the workspace and its entries marked in the same pass (fill_sparse_small_kernel<.., true>);
 // otherwise the caller's arrays are marked and checked (mark_check_kernel): with
@@ -1479,9 +1628,12 @@ static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, co
                                   rocprim::plus<int32_t>(), s);
     if (err != hipSuccess) return err;
     const size_t gen_bytes = gen ? n * (2 * sizeof(int64_t) + sizeof(double)) + 64 : 0;
+    // a claimed filled operator (no host wait): the gated fallback's CSR (ptr, cursors, buckets)
+    const bool gated = !gen && p.arrays_filled;
+    const size_t fb_bytes = gated ? (size_t)(2 * p.M + 1) * sizeof(int32_t) + n * sizeof(int32_t) + 64 : 0;
     const size_t bytes = (size_t)NV * 4 * mw + (size_t)NGT * sizeof(int32_t) + (size_t)NV * sizeof(int32_t) +
                          (size_t)(NGT + 1) * sizeof(int32_t) + nrec * sizeof(uint32_t) + scan_bytes + gen_bytes + 512 +
-                         16;
+                         16 + fb_bytes;
     char *ws = nullptr;
     err = ws_alloc((void **)&ws, bytes, s);
     if (err != hipSuccess) return err;
@@ -1500,6 +1652,12 @@ static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, co
         int64_t *gc = (int64_t *)carve(n * sizeof(int64_t));
         double *gv = (double *)carve(n * sizeof(double));
         rows = gr; cols = gc; vals = gv;
+    }
+    int32_t *fb_ptr = nullptr, *fb_cur = nullptr, *fb_bkt = nullptr;
+    if (gated) {
+        fb_ptr = (int32_t *)carve((size_t)(p.M + 1) * sizeof(int32_t));
+        fb_cur = (int32_t *)carve((size_t)p.M * sizeof(int32_t));
+        fb_bkt = (int32_t *)carve(n * sizeof(int32_t));
     }
     const uint32_t kmul = y_k ? (uint32_t)sizeof(double) : (uint32_t)(SU_J * sizeof(double));
     err = hipMemsetAsync(mask, 0, mask_b, s);
@@ -1559,6 +1717,20 @@ static hipError_t run_sparse_dma(const SparseApply &p0, const SparseGen *gen, co
                                 nrb_u, vec_out, chk);
         err = hipGetLastError();
         timing_end(s);
+    }
+    if (err == hipSuccess && gated) {   // the fallback, gated on the check's flag (section 7b)
+        uint32_t *hf = fb_host_slot();
+        hipLaunchKernelGGL(fb_bucket_kernel, dim3(1), dim3(FB_NT), 0, s, bad, nnz, rows, cols, p, fb_ptr, fb_cur,
+                           fb_bkt, hf);
+        err = hipGetLastError();
+        if (err == hipSuccess) {
+            const int64_t tiles = ((p.M + 63) / 64) * p.N;
+            const int64_t blocks = (tiles + 3) / 4 < 2048 ? (tiles + 3) / 4 : 2048;
+            hipLaunchKernelGGL(fb_apply_kernel, dim3((unsigned)blocks), dim3(256), 0, s, bad, rows, cols, vals, p,
+                               fb_ptr, fb_bkt);
+            err = hipGetLastError();
+        }
+        if (err == hipSuccess) g_sparse_path = SPARSE_PATH_DMA_GATED;
     }
     hipError_t e2 = ws_free(ws, s);
     return err != hipSuccess ? err : e2;

@@ -29,8 +29,9 @@ struct SparseApply {
     int kcs;         // LDS-DMA apply (saso.hip section 5): log2 of its chunk depth; set by the apply itself
     // Caller's COO arrays (rbh_options.sparse_filled): 0 = of unknown origin -- the LDS-DMA apply
     // takes them after a device check (every in-window alpha*v is +-1, no duplicate (row, k)) that
-    // the host waits for; 1 = fill_sparse's output for this operator, unmodified -- the same check
-    // runs on the device without a wait, and a failed check makes the apply write NaN.
+    // the host waits for; 1 = claimed fill_sparse's output for this operator, unmodified -- the same
+    // check runs on the device without a wait; if it fails, the DMA apply writes nothing and a
+    // fallback gated on the check's flag computes C from the arrays (saso.hip section 7b).
     int arrays_filled;
 };
 
@@ -48,8 +49,12 @@ hipError_t run_sparse_sampled_f32(const SparseApply &p, const SparseGen &g, int6
 // The apply a sparse sketch ran (rbh_sparse_last_path): none (empty), the LDS-DMA kernel on the
 // sort-free CSR, the row gather, the sorted CSR with the uniform-value kernel (its general kernel
 // takes over for mixed values), or the general kernel.
+// A claimed filled operator (arrays_filled, no host wait) reports DMA when its device check passed,
+// FALLBACK when it failed and the gated fallback wrote C (saso.hip section 7b), PENDING while the stream
+// has not yet run the call; DMA_GATED is internal (resolved to one of those three).
 enum SparsePath : int { SPARSE_PATH_NONE = 0, SPARSE_PATH_DMA = 1, SPARSE_PATH_GATHER = 2, SPARSE_PATH_SORTED_UNIT = 3,
-                        SPARSE_PATH_SORTED = 4 };
+                        SPARSE_PATH_SORTED = 4, SPARSE_PATH_FALLBACK = 5, SPARSE_PATH_PENDING = 6,
+                        SPARSE_PATH_DMA_GATED = 100 };
 int sparse_last_path();
 
 // CSR/CSC pointer array (n_major + 1 entries) -> the major index of every entry (saso.hip).

@@ -554,6 +554,7 @@ static void filled_operator_fast_path() {
     std::vector<double> Bd(d * n);
     for (int rep = 0; rep < 2; ++rep) {
         RandBLAS::sketch_general(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, m, 1.0, Sd, dA, m, 0.0, dB, d);
+        CHECK(hipDeviceSynchronize() == hipSuccess);   // (the claimed call decides its path on the device)
         CHECK(rbh_sparse_last_path() == 1);
         CHECK(hipMemcpy(Bd.data(), dB, d * n * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess);
         for (int64_t e = 0; e < d * n; ++e) CHECK(Bd[e] == B1[e]);
@@ -573,6 +574,32 @@ static void filled_operator_fast_path() {
     CHECK(rbh_sparse_last_path() == 1);
     CHECK(hipMemcpy(Bd.data(), dB, d * n * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess);
     for (int64_t e = 0; e < d * n; ++e) CHECK(Bd[e] == B1[e]);
+
+    // values rescaled in place with the claim left standing (isometry scaling,
+    // sparse_skops.hh:167-177), applied with alpha = 1. The device check fails; the fast apply writes
+    // nothing and the fallback gated on the check's flag computes B (path 5): +-1/2 gives B1 / 2
+    // exactly, and +-0.3 gives the checked (unclaimed) path's bits on the same arrays.
+    Sd.filled_by_library = true;   // values +-1/2 now: a false claim
+    RandBLAS::sketch_general(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, m, 1.0, Sd, dA, m, 0.0, dB, d);
+    CHECK(hipDeviceSynchronize() == hipSuccess);
+    CHECK(rbh_sparse_last_path() == 5);
+    CHECK(hipMemcpy(Bd.data(), dB, d * n * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess);
+    for (int64_t e = 0; e < d * n; ++e) CHECK(Bd[e] == 0.5 * B1[e]);
+    CHECK(hipMemcpy(hv.data(), dv, nnz * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess);
+    for (auto &v : hv) v = v > 0 ? 0.3 : -0.3;
+    CHECK(hipMemcpy(dv, hv.data(), nnz * sizeof(double), hipMemcpyHostToDevice) == hipSuccess);
+    RandBLAS::sketch_general(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, m, 1.0, Sd, dA, m, 0.0, dB, d);
+    CHECK(hipDeviceSynchronize() == hipSuccess);
+    CHECK(rbh_sparse_last_path() == 5);
+    std::vector<double> Bg(d * n);
+    CHECK(hipMemcpy(Bg.data(), dB, d * n * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess);
+    Sd.filled_by_library = false;
+    RandBLAS::sketch_general(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, m, 1.0, Sd, dA, m, 0.0, dB, d);
+    CHECK(rbh_sparse_last_path() == 3 || rbh_sparse_last_path() == 4);
+    CHECK(hipMemcpy(Bd.data(), dB, d * n * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess);
+    int64_t nz = 0;
+    for (int64_t e = 0; e < d * n; ++e) { CHECK(Bg[e] == Bd[e]); nz += Bd[e] != 0.0; }
+    CHECK(nz > d * n / 2);
     (void)hipFree(dr); (void)hipFree(dc); (void)hipFree(dv); (void)hipFree(dA); (void)hipFree(dB);
 }
 
