@@ -1397,18 +1397,22 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     // part p contracts the lane's values v = PV p .. PV p + PV - 1 (its 16-B slots 2 g + NLD p + l,
     // l < NLD); the ring holds part-blocks
     hv_t mv[NSLOT];
-    auto mload = [&](int slot, int i, int64_t kt, const TriStep &ts_) {   // part-block i = p FB + c of step kt
+    // One-triangle operands (TRI 1-4) stream in runs of rounds (round 6), uniform per wave: rounds
+    // whose part-blocks (and the next step's, which their last step prefetches) all lie inside the
+    // stored triangle run MODE_IN, rounds whose part-blocks are all mirrored MODE_MIR, and the one or
+    // two rounds that cross the wave's diagonal MODE_GEN, which picks each part-block's class (round 5
+    // did that for every part-block: SALU 7.5x the full-storage kernel's). Each mode is its own loop
+    // (below): a class branch per step made the register allocator spill a kilobyte a lane. Every class
+    // issues PV 8-B loads into the same ring registers; TRI 5 is always MODE_MIR.
+    constexpr int MODE_GEN = 0, MODE_IN = 1, MODE_MIR = 2;
+    auto mload = [&](auto mode, int slot, int i, int64_t kt, const TriStep &ts_) __attribute__((always_inline)) {   // part-block i = p FB + c of step kt
+        constexpr int MODE = decltype(mode)::value;
         const uint32_t soff = (uint32_t)(kt * 128);
         if constexpr (TRI != 0) {
-            // one 16-B load whatever the class, its resource and offsets picked by selects on the
-            // uniform class: control flow here (the per-element straddle loads of round 4) left the
-            // compiler unable to count the prefetch ring's loads, and it waited for each one at once
-            // (vmcnt(0)/(1) where the plain kernel waits with vmcnt(7))
-            // PV one-value loads whatever the class (inline asm: the compiler sees no VMEM in this
-            // loop, so it neither waits on them nor miscounts a ring whose classes differ; the
-            // consumer waits, counting them). (Round 5: the in-triangle and diagonal part-blocks as
-            // 16-B loads, with the consumer's count picked per class by uniform branches, took C5p
-            // 4.27 -> 4.89 ms: the branches cost more than the loads saved.)
+            // inline asm loads: the compiler sees no VMEM in this loop, so it neither waits on them nor
+            // miscounts a ring whose classes differ; the consumer waits, counting them (vm_wait_n).
+            // (Round 5: every class as PV 8-B loads with the class picked per part-block: C5p 4.26 ms;
+            // 16-B inside / diagonal loads with per-part-block branches and counts: 4.89 ms.)
             const int c = i % FB, pp = i / FB;
             typedef T tv_t[PV];
             tv_t &dst = *reinterpret_cast<tv_t *>(&mv[slot]);
@@ -1418,7 +1422,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
                 else
                     asm volatile("buffer_load_dword %0, %1, %2, %3 offen" : "=v"(o) : "v"(vo), "s"(rs_), "s"(so) : "memory");
             };
-            if (is_mir(ts_, c)) {   // mirrored: down the stored rows, at the lane's own position
+            auto mirrored = [&]() {   // down the stored rows, at the lane's own position
                 const uint32_t so_ = ts_.so_mir + (uint32_t)(16 * c * (int)sizeof(T));
                 // stored rows at a fixed stride (full storage, TRI 1 / 2 / 5): value pe's row offset
                 // pe tso is uniform (soffset), one offset VGPR for all; packed rows: one per value
@@ -1429,15 +1433,28 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
                     if (LIN) ld8(dst[e], ts_.mr[0], mrs4, so_ + (uint32_t)pe * tso * (uint32_t)sizeof(T));
                     else ld8(dst[e], ts_.mr[pe], mrs4, so_);
                 }
-            } else if constexpr (TRI == 5) {
+            };
+            // inside the triangle: the lane's own values, as full storage, as PV 8-B loads into the same
+            // ring registers every class writes (a 16-B load writes them as one register tuple, and where
+            // paths write a ring slot in different forms the compiler merges them with copies -- made
+            // before the loads land)
+            auto inside = [&]() {
+                const uint32_t so_ = ts_.so_in + (uint32_t)(8 * PV * pp);
+#pragma unroll
+                for (int e = 0; e < PV; ++e) ld8(dst[e], voff[c], mrs4, so_ + 8u * e);
+            };
+            if constexpr (TRI == 5 || MODE == MODE_MIR) {
+                mirrored();
+            } else if constexpr (MODE == MODE_IN) {
+                inside();
+            } else if (is_mir(ts_, c)) {
+                mirrored();
             } else if (c == ts_.cd) {   // the diagonal block, from the workspace
                 const uint32_t so_ = ts_.so_dia + (uint32_t)(8 * PV * pp);
 #pragma unroll
                 for (int e = 0; e < PV; ++e) ld8(dst[e], vdiag, drs4, so_ + 8u * e);
-            } else {   // inside the triangle: the lane's own values, as full storage
-                const uint32_t so_ = ts_.so_in + (uint32_t)(8 * PV * pp);
-#pragma unroll
-                for (int e = 0; e < PV; ++e) ld8(dst[e], voff[c], mrs4, so_ + 8u * e);
+            } else {
+                inside();
             }
             return;
         }
@@ -1541,12 +1558,14 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     if (kt0 < kt1) {
         const TriStep t0 = tri_step(kt0);
 #pragma unroll
-        for (int i = 0; i < PF; ++i) mload(i % NSLOT, CMAJOR ? seq_block(i) : i, kt0, t0);
+        for (int i = 0; i < PF; ++i) mload(std::integral_constant<int, MODE_GEN>{}, i % NSLOT, CMAJOR ? seq_block(i) : i, kt0, t0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
     const int64_t nrounds = (kt1 - kt0 + R - 1) / R;
-    for (int64_t rd = 0; rd < nrounds; ++rd) {
+    // one round of R steps in mode rmode (one-triangle operands: every part-block of the round's steps
+    // and of the step after them in the same class, or MODE_GEN; the loops below)
+    auto do_round = [&](auto rmode, int64_t rd) __attribute__((always_inline)) {
         const int half = (int)(rd & 1);
         const int64_t kr0 = kt0 + rd * R;
         if (rd > 0) rebase(kr0);   // (the loads already issued keep the resource they were issued with)
@@ -1571,7 +1590,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
                     for (int h = 0; h < NPART; ++h) {
                         const int s = c * NPART + h, sn = s + PF;
                         const int64_t ktn = sn < NH ? kt : (kt + 1 < kt1 ? kt + 1 : kt);
-                        mload(sn % NSLOT, seq_block(sn % NH), ktn, tsn);
+                        mload(std::integral_constant<int, MODE_GEN>{}, sn % NSLOT, seq_block(sn % NH), ktn, tsn);
                         // keep the load here, PF part-blocks ahead of its use (the scheduler otherwise
                         // sinks it next to its MFMAs and waits on it at once)
                         __builtin_amdgcn_sched_barrier(0);
@@ -1584,6 +1603,10 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
                                                : Mfma<T>::mma(gf[h][a][e], m[e], acc[a][c]);
                     }
             } else {
+            // one step in mode MODE (one-triangle operands, above; TRI 0 ignores it)
+            auto run_step = [&](auto mode) __attribute__((always_inline)) {
+                constexpr int MODE = decltype(mode)::value;
+                constexpr int WAIT = PV * PF;   // (every class: PV loads a part-block)
 #pragma unroll
             for (int h = 0; h < NPART; ++h) {
                 hv_t gf[FA];
@@ -1594,18 +1617,18 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
                     // part-block i + PF (this step's, or the next step's first ones), PF ahead
                     const int i = h * FB + c, in = i + PF;
                     const int64_t ktn = in < NH ? kt : (kt + 1 < kt1 ? kt + 1 : kt);
-                    mload(in % NSLOT, in % NH, ktn, in < NH ? tsc : tsn);
+                    mload(mode, in % NSLOT, in % NH, ktn, in < NH ? tsc : tsn);
                     __builtin_amdgcn_sched_barrier(0);   // (as above)
                     hv_t m;
                     if constexpr (TRI == 0) {
                         m = mv[i % NSLOT];
                     } else {
-                        // the part-block's PV loads have landed once at most the PV PF issued after
-                        // them are in flight (PV per part-block, in order); then the ring registers
-                        // pass through one empty asm the MFMAs read, so nothing reads them earlier
+                        // the part-block's loads have landed once at most the WAIT loads issued after
+                        // them are in flight (in order); then the ring registers pass through one empty
+                        // asm the MFMAs read, so nothing reads them earlier
                         typedef T tv_t[PV];
                         tv_t &src = *reinterpret_cast<tv_t *>(&mv[i % NSLOT]);
-                        vm_wait_n<PV * PF>();
+                        vm_wait_n<WAIT>();
                         vm_fence(src);
 #pragma unroll
                         for (int e = 0; e < PV; ++e) m[e] = src[e];
@@ -1617,6 +1640,8 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
                             acc[a][c] = GX ? Mfma<T>::mma(m[e], gf[a][e], acc[a][c]) : Mfma<T>::mma(gf[a][e], m[e], acc[a][c]);
                 }
             }
+            };
+            run_step(rmode);
             }
             // the next round's generated tiles: every wave's share, spread over the round (f64: its
             // one call after step 1; f32: one call after every step)
@@ -1627,6 +1652,26 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
+    if constexpr (TRI >= 1 && TRI <= 4) {
+        // A wave's steps fall in three runs: every part-block on the stored side (steps kt < W for
+        // k <= o storage, W = wm0 / 16), the FB steps that cross its diagonal, every part-block mirrored
+        // (kt >= W + FB); reversed for k >= o storage. Each run of whole rounds (a round's last step
+        // prefetches the next step's part-blocks, so it counts too) gets its own loop and mode; rounds
+        // that touch the crossing run MODE_GEN. Every wave still runs nrounds rounds (one barrier each).
+        // ra: the rounds whose steps kr0 .. kr0 + R all lie below W; rb: the first round with kr0 >= W + FB
+        const int64_t W = wm0 / 16, hi_from = W + FB;
+        int64_t ra = W - R - 1 - kt0 >= 0 ? (W - R - 1 - kt0) / R + 1 : 0;
+        ra = ra < nrounds ? ra : nrounds;
+        int64_t rb = hi_from - kt0 > 0 ? (hi_from - kt0 + R - 1) / R : 0;
+        rb = rb < ra ? ra : (rb > nrounds ? nrounds : rb);
+        constexpr int FIRST = TKLE ? MODE_IN : MODE_MIR, LAST = TKLE ? MODE_MIR : MODE_IN;
+        int64_t rd = 0;
+        for (; rd < ra; ++rd) do_round(std::integral_constant<int, FIRST>{}, rd);
+        for (; rd < rb; ++rd) do_round(std::integral_constant<int, MODE_GEN>{}, rd);
+        for (; rd < nrounds; ++rd) do_round(std::integral_constant<int, LAST>{}, rd);
+    } else {
+        for (int64_t rd = 0; rd < nrounds; ++rd) do_round(std::integral_constant<int, MODE_MIR>{}, rd);
     }
 
     // the one-triangle loads the compiler cannot see: the last (clamped) ones land before the
