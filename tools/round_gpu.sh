@@ -8,8 +8,8 @@ cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 what="${*:-tests bench prof pmc}"
-CONFIGS="${CONFIGS:-c2 c1 ns c3 c4 c5 c5p}"
-PMC_CONFIGS="${PMC_CONFIGS:-c2 c3 c4}"
+CONFIGS="${CONFIGS:-ns c2 c1 c3 c4 c4full c5 c5p}"
+PMC_CONFIGS="${PMC_CONFIGS:-ns c2 c3 c4 c4full c5 c5p c1}"
 
 run() {   # run <log> <timeout> <cmd...>
     local logf="$1" tmo="$2"; shift 2

@@ -20,7 +20,8 @@ sys.path.insert(0, ROOT)
 CONFIGS = {   # bench.py CONFIGS: (kind, dtype, d, m, n, vec_nnz)
     "c1": ("dense", "f64", 128, 4096, 4096, 0), "c2": ("dense", "f64", 1024, 16384, 16384, 0),
     "ns": ("dense", "f64", 2048, 16384, 16384, 0), "c3": ("saso", "f64", 1024, 16384, 16384, 8),
-    "c4": ("dense", "f32", 256, 32768, 32768, 0), "c5": ("sksy", "f64", 512, 16384, 16384, 0),
+    "c4": ("dense", "f32", 256, 32768, 32768, 0), "c4full": ("dense", "f32", 2048, 32768, 32768, 0),
+    "c5": ("sksy", "f64", 512, 16384, 16384, 0),
     "c5p": ("sksyp", "f64", 512, 16384, 16384, 0)}
 PEAK = {"f64": 78.6e12, "f32": 157.3e12}
 HBM_PEAK = 8.0e12
