@@ -174,7 +174,8 @@ typedef struct rbh_options {
  * 2 generic GEMM, 3 fused GEMM, 4 wide f64 GEMM, 5 wide f32 GEMM (32-deep), 6 wide one-triangle
  * GEMM, 7 triangle expanded, then the plain kernels, 8 streamed GEMM (the default for the wide
  * kernels' problems), 9 streamed one-triangle GEMM, 10 streamed GEMM on a memory operand contiguous
- * along its outer index (f64: A in a RowMajor left or ColMajor right sketch); its output tiles,
+ * along its outer index (f64: A in a RowMajor left or ColMajor right sketch), 11 split-K gemv with the
+ * operator drawn in the kernel (one operand a single vector: sketch_vector); its output tiles,
  * split-K factor and workgroups (tiles * splitk). */
 typedef struct rbh_plan {
     int32_t kernel;

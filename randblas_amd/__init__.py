@@ -298,7 +298,7 @@ class Options:
 
 
 PLAN_KERNELS = {0: "none", 1: "scale", 2: "generic", 3: "fused", 4: "wide", 5: "wide32", 6: "wide_tri",
-                7: "symmetrize", 8: "stream", 9: "stream_tri", 10: "stream_t"}
+                7: "symmetrize", 8: "stream", 9: "stream_tri", 10: "stream_t", 11: "gemv"}
 
 
 @dataclass

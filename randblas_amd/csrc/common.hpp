@@ -83,6 +83,7 @@ enum PlanKernel : int {
     PLAN_STREAM = 8,      // skge_stream_kernel (the wide kernels' sums; f64 64 x 512, f32 32 / 64 x 1024)
     PLAN_STREAM_TRI = 9,  // skge_stream_kernel with a one-triangle symmetric operand (f64)
     PLAN_STREAM_T = 10,   // skge_stream_kernel<TRI 5>: memory operand contiguous along o (f64)
+    PLAN_GEMV = 11,       // skve.hip: the memory operand is one vector (sketch_vector), split-K gemv
 };
 struct GemmPlan {
     int kernel;
@@ -97,6 +98,13 @@ GemmPlan plan_gemm_f32(const GemmProblem &p);
 // out[o*n + k] (skge_dense.hip); the fallback when the fused one-triangle kernel does not apply.
 hipError_t launch_symmetrize_f64(int tri, const double *A, int64_t lda, int64_t n, double *out, hipStream_t s);
 hipError_t launch_symmetrize_f32(int tri, const float *A, int64_t lda, int64_t n, float *out, hipStream_t s);
+
+// The vector problems (skve.hip): M == 1 with X in memory or N == 1 with Y in memory, the other
+// operand generated (sketch_vector, skve.hh:152-176)
+bool gemv_ok(const GemmProblem &p);
+int gemv_split(const GemmProblem &p);
+hipError_t launch_gemv_f64(const GemmProblem &p, hipStream_t s);
+hipError_t launch_gemv_f32(const GemmProblem &p, hipStream_t s);
 
 // Kernel launchers (skge_dense.hip)
 hipError_t launch_gemm_f64(const GemmProblem &p, hipStream_t s);

@@ -2255,6 +2255,13 @@ static GemmPlan plan_gemm(const GemmProblem &p) {
     GemmPlan pl{PLAN_NONE, 1, 0, 0};
     if (p.M <= 0 || p.N <= 0) return pl;
     if (p.K <= 0 || p.alpha == 0.0) { pl.kernel = PLAN_SCALE; return pl; }
+    if (!p.tri && gemv_ok(p)) {   // one vector operand: sketch_vector (skve.hip)
+        pl.kernel = PLAN_GEMV;
+        pl.splitk = gemv_split(p);
+        pl.tiles = p.M == 1 ? p.N : p.M;
+        pl.workgroups = pl.tiles * pl.splitk;
+        return pl;
+    }
     auto wide_tiles = [&]() {
         const bool gx = p.xkind != MEM;
         const int64_t gnO = gx ? p.M : p.N, mnO = gx ? p.N : p.M;
@@ -2317,6 +2324,7 @@ static hipError_t launch_gemm(const GemmProblem &p, hipStream_t s) {
     if (p.tri) return launch_gemm_tri<T>(p, s);
     const bool unif = (p.xkind != MEM ? p.xg.family : p.yg.family) == rb::UNIFORM;
     const int kernel = plan_gemm<T>(p).kernel;
+    if (kernel == PLAN_GEMV) return sizeof(T) == 8 ? launch_gemv_f64(p, s) : launch_gemv_f32(p, s);
     if (kernel == PLAN_STREAM) {
 #define RBH_STREAM_L(GK, GX)                                                                   \
     return unif ? launch_stream<T, GK, rb::UNIFORM, GX>(p, s) : launch_stream<T, GK, rb::GAUSSIAN, GX>(p, s)

@@ -187,6 +187,20 @@ def test_spill_guard_reads_the_compiler_remarks(tmp_path):
         assert subprocess.run([sys.executable, tool, f], capture_output=True).returncode == 0, f
 
 
+def test_plan_vector_problems_take_gemv():
+    """sketch_vector (sketch_general RowMajor with n = 1) is a gemv with the operator drawn in the
+    kernel (plan "gemv", skve.hip), split over K for the whole chip; a one-column ColMajor sketch too."""
+    for dtype in ("f64", "f32"):
+        for SR, SC, opS in ((1024, 16384, "N"), (16384, 1024, "T"), (16384, 1024, "N")):
+            S = rb.DenseSkOp(rb.DenseDist(SR, SC), rb.RNGState(0))
+            d, m = (SR, SC) if opS == "N" else (SC, SR)
+            pl = rb.plan_left("R", opS, "N", d, 1, m, S, 256, 1, 1, dtype=dtype)
+            assert pl.kernel == "gemv" and pl.tiles == d and 1 <= pl.splitk <= max(1, m // 1024), (SR, SC, opS, pl)
+        S = rb.DenseSkOp(rb.DenseDist(512, 8192), rb.RNGState(0))
+        assert rb.plan_left("C", "N", "N", 512, 1, 8192, S, 256, 8192, 512, dtype=dtype).kernel == "gemv"
+        assert rb.plan_left("C", "N", "N", 512, 2, 8192, S, 256, 8192, 512, dtype=dtype).kernel != "gemv"
+
+
 def test_plan_options_fix_the_split():
     assert _plan(128, 4096, 4096, opts=rb.Options(splitk=1)).splitk == 1
     assert _plan(128, 4096, 4096, opts=rb.Options(splitk=3)) == rb.Plan("stream", 3, 16, 48)

@@ -158,3 +158,39 @@ def test_sketch_vector_full(cuda):
     dy2 = dev(np.zeros(d), cuda)
     rb.sketch_vector("N", d, m, 1.0, S, dev(x, cuda), 1, 0.0, dy2, 1)
     assert np.array_equal(host(dy), host(dy2))
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+@pytest.mark.parametrize("opS", ["N", "T"])
+@pytest.mark.parametrize("shape", [(1024, 16384), (16384, 1024), (300, 70001)])
+def test_sketch_vector_gemv_kernel(cuda, dtype, opS, shape):
+    """Round 6: a vector operand takes the split-K gemv kernel (plan "gemv", skve.hip) instead of the
+    tile kernels (5.5 ms at d = 1024, m = 16384 on the generic kernel's 8 tiles). Both Philox
+    orientations (wide and tall operators, S and S^T), strided x and y, alpha and beta, f64 and f32:
+    within the reference's componentwise bound of the oracle-filled operator's gemv."""
+    d, m = shape
+    incx, incy, alpha, beta = 2, 3, -0.75, 0.5
+    npdt, tdt = (np.float64, torch.float64) if dtype == "f64" else (np.float32, torch.float32)
+    eps = np.finfo(npdt).eps
+    SR, SC = (d, m) if opS == "N" else (m, d)
+    S = rb.DenseSkOp(rb.DenseDist(SR, SC), rb.RNGState(5))
+    nx, ny = (m, d)
+    x = O.random_matrix(nx, 1, 31).astype(npdt).astype(np.float64)
+    y0 = O.random_matrix(ny, 1, 32).astype(npdt).astype(np.float64)
+    xs, ys = strided(x, incx), strided(y0, incy)
+    dx = torch.from_numpy(xs.astype(npdt)).to(cuda)
+    dy = torch.from_numpy(ys.astype(npdt)).to(cuda)
+    pl = rb.plan_left("R", opS, "N", d, 1, m, S, dx, incx, incy, dtype=dtype)
+    assert pl.kernel == "gemv", pl
+    # (d, m) of sketch_vector are submat(S)'s dimensions before op (skve.hh:152-176)
+    rb.sketch_vector(opS, SR, SC, alpha, S, dx, incx, beta, dy, incy)
+    Sm = dense_op(SR, SC, 5)
+    opm = Sm if opS == "N" else Sm.T
+    exp = alpha * (opm @ x) + beta * y0
+    bound = abs(alpha) * m * 2 * eps * (np.abs(opm) @ np.abs(x)) + abs(beta) * eps * np.abs(y0) + 4 * eps * np.abs(exp)
+    got = host(dy).astype(np.float64)
+    y = got[::incy]
+    assert np.all(np.abs(y - exp) <= bound), f"max err {np.max(np.abs(y - exp) - bound)}"
+    gaps = np.ones(len(got), bool)
+    gaps[::incy] = False
+    assert np.all(np.isnan(got[gaps]))
