@@ -69,7 +69,16 @@ def sparse(d, m, n, dens):
                       "apply": rb.sparse_last_path()}), flush=True)
 
 
+def filld(d, m, layout):
+    buf = torch.empty(d * m, dtype=torch.float64, device=dev)
+    t = timed(lambda: rb.fill_dense(layout, rb.DenseDist(d, m), d, m, 0, 0, buf, rb.RNGState(0)))
+    print(json.dumps({"path": "fill_dense", "layout": layout, "d": d, "m": m, "ms": t,
+                      "entries_per_s": d * m / (t * 1e-3), "hbm_write_frac": d * m * 8 / (t * 1e-3) / HBM}), flush=True)
+
+
 if __name__ == "__main__":
+    for layout in ("R", "C"):
+        filld(4096, 65536, layout)
     for d, m in ((1024, 16384), (2048, 65536), (4096, 262144)):
         vector(d, m)
     for d, m, n, dens in ((1024, 16384, 16384, 1e-3), (1024, 16384, 16384, 1e-2), (256, 65536, 8192, 1e-3)):
