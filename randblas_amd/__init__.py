@@ -378,7 +378,11 @@ def fill_sparse(S: SparseSkOp, rows, cols, vals, stream=None) -> None:
 
 def _array_versions(S):
     """(identity, in-place version) of S's three arrays: torch counts every in-place write of a
-    tensor in `_version`, so a changed tuple means the arrays are no longer fill_sparse's output."""
+    tensor in `_version`, so a changed tuple means the arrays are no longer fill_sparse's output.
+    Writes torch does not count (raw device pointers, DLPack views, other libraries) leave the claim
+    standing; the result is still right: the library checks the arrays on the device, and when the
+    check fails the fast apply writes nothing and a fallback gated on the check computes B
+    (rbh_sparse_last_path 5). A missed write only costs the fast apply's discarded work."""
     return tuple((id(a), getattr(a, "_version", None)) for a in (S.rows, S.cols, S.vals))
 
 

@@ -1151,6 +1151,9 @@ int sksy_overlapped(GemmProblem p, char layout, const T *dA, int64_t n, int64_t 
     *done = false;
     *flags = 0;
     if (p.M <= 0 || p.N <= 0 || p.K <= 0 || p.alpha == 0.0) return RBH_OK;
+    // W is M x N: past 1 GiB the sequential check-then-sketch path runs instead (the arena keeps
+    // what it hands out)
+    if ((double)p.M * (double)p.N * sizeof(T) > (double)(1ull << 30)) return RBH_OK;
     hipStream_t s2;
     hipEvent_t fork, join;
     RBH_HIP(side_stream(&s2, &fork, &join));
@@ -1170,15 +1173,30 @@ int sksy_overlapped(GemmProblem p, char layout, const T *dA, int64_t n, int64_t 
     p.ldc = p.M;
     p.beta = 0.0;
     p.beside = 1;   // the check's waves need 32 registers a SIMD lane beside the GEMM's
-    RBH_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
-    RBH_HIP(hipEventRecord(fork, s));
-    RBH_HIP(launch_gemm_t<T>(p, s));           // the sketch first: its workgroups take the CUs
-    RBH_HIP(hipStreamWaitEvent(s2, fork, 0));
-    RBH_HIP(launch_sym_lean_t<T>(layout, dA, n, lda, tol, flag, s2));
-    RBH_HIP(hipEventRecord(join, s2));
-    RBH_HIP(hipStreamWaitEvent(s, join, 0));
-    RBH_HIP(launch_commit_t<T>(p.M, p.N, W, beta, C, ldc, flag, s));
-    RBH_HIP(hipMemcpyAsync(flags, flag, sizeof(int), hipMemcpyDeviceToHost, s));
+    // Once the workspaces exist every failure goes through here: both streams drained (the side
+    // stream may still be reading A for the check), then W and the flag returned to the arena.
+#define RBH_HIP_OV(expr)                                                                              \
+    do {                                                                                              \
+        hipError_t e_ = (expr);                                                                       \
+        if (e_ != hipSuccess) {                                                                       \
+            (void)hipStreamSynchronize(s2);                                                           \
+            (void)hipStreamSynchronize(s);                                                            \
+            (void)ws_free(W, s);                                                                      \
+            (void)ws_free(flag, s);                                                                   \
+            return set_error(RBH_ERR_HIP, "HIP error %s (%d) at %s:%d: %s", hipGetErrorName(e_), (int)e_, \
+                             __FILE__, __LINE__, #expr);                                              \
+        }                                                                                             \
+    } while (0)
+    RBH_HIP_OV(hipMemsetAsync(flag, 0, sizeof(int), s));
+    RBH_HIP_OV(hipEventRecord(fork, s));
+    RBH_HIP_OV(launch_gemm_t<T>(p, s));           // the sketch first: its workgroups take the CUs
+    RBH_HIP_OV(hipStreamWaitEvent(s2, fork, 0));
+    RBH_HIP_OV(launch_sym_lean_t<T>(layout, dA, n, lda, tol, flag, s2));
+    RBH_HIP_OV(hipEventRecord(join, s2));
+    RBH_HIP_OV(hipStreamWaitEvent(s, join, 0));
+    RBH_HIP_OV(launch_commit_t<T>(p.M, p.N, W, beta, C, ldc, flag, s));
+    RBH_HIP_OV(hipMemcpyAsync(flags, flag, sizeof(int), hipMemcpyDeviceToHost, s));
+#undef RBH_HIP_OV
     RBH_HIP(ws_free(W, s));
     RBH_HIP(ws_free(flag, s));
     RBH_HIP(hipStreamSynchronize(s));
