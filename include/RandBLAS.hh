@@ -2,7 +2,7 @@
 //
 // A program written against RylieWeaver/RandBLAS (snapshot 2024-10-08) for this path compiles
 // unchanged against this header: it provides the reference's types and overloads
-//   RNGState<r123::Philox4x32> (RandBLAS/base.hh:161-232), MajorAxis (base.hh:138-150),
+//   RNGState<r123::Philox4x32 | r123::Threefry4x32> (RandBLAS/base.hh:153-232), MajorAxis (base.hh:138-150),
 //   DenseDistName / DenseDist / DenseSkOp (dense_skops.hh:204-419), fill_dense x3 (:486-592),
 //   SparseDist / SparseSkOp / fill_sparse (sparse_skops.hh:134-413),
 //   sketch_general x8 (skge.hh:771-1214), sketch_symmetric x4 (sksy.hh:165-537),
@@ -18,7 +18,8 @@
 //
 // A DenseSkOp whose buff is nullptr is regenerated from its Philox counters inside the fused MFMA
 // GEMM, tile by tile into LDS; it is not written to memory (unless the thread's options,
-// ext::ScopedOptions, ask for the window to be drawn into a workspace first).
+// ext::ScopedOptions, ask for the window to be drawn into a workspace first). A
+// Threefry operator's window is always drawn into a workspace first and applied from it.
 // fill_dense(S) and submatrix_as_blackbox still fill a host buffer, as in the reference, after
 // which the operator is applied from it.
 #pragma once
@@ -46,7 +47,8 @@ enum class Side : char { Left = 'L', Right = 'R' };
 }  // namespace blas
 
 // ---------------------------------------------------------------------------------------------
-// Random123's Philox4x32 interface as RandBLAS uses it (ctr_type / key_type with incr, operator())
+// Random123's Philox4x32 / Threefry4x32 interface as RandBLAS uses it (ctr_type / key_type with
+// incr, operator())
 // ---------------------------------------------------------------------------------------------
 namespace r123 {
 template <int N>
@@ -79,6 +81,31 @@ struct Philox4x32 {
             const ctr_type n = {{(uint32_t)(p1 >> 32) ^ c.v[1] ^ k.v[0], (uint32_t)p1,
                                  (uint32_t)(p0 >> 32) ^ c.v[3] ^ k.v[1], (uint32_t)p0}};
             c = n;
+        }
+        return c;
+    }
+};
+
+// Threefry4x32-20 (Random123 threefry.h): RNGState<r123::Threefry4x32> selects the device's
+// Threefry generator (rbh_state.rng = RBH_RNG_THREEFRY4X32)
+struct Threefry4x32 {
+    using ctr_type = U32Array<4>;
+    using key_type = U32Array<4>;
+    ctr_type operator()(ctr_type c, key_type k) const {
+        static const int rot[8][2] = {{10, 26}, {11, 21}, {13, 27}, {23, 5}, {6, 20}, {17, 11}, {25, 10}, {18, 20}};
+        const uint32_t ks[5] = {k.v[0], k.v[1], k.v[2], k.v[3], 0x1BD11BDAu ^ k.v[0] ^ k.v[1] ^ k.v[2] ^ k.v[3]};
+        auto rotl = [](uint32_t x, int r) { return (x << r) | (x >> (32 - r)); };
+        for (int i = 0; i < 4; ++i) c.v[i] += ks[i];
+        for (int r = 0; r < 20; ++r) {
+            const int *R = rot[r % 8];
+            const int a = r % 2 ? 3 : 1, b = r % 2 ? 1 : 3;   // (the mix pairs alternate)
+            c.v[0] += c.v[a]; c.v[a] = rotl(c.v[a], R[0]) ^ c.v[0];
+            c.v[2] += c.v[b]; c.v[b] = rotl(c.v[b], R[1]) ^ c.v[2];
+            if (r % 4 == 3) {
+                const uint32_t s = (uint32_t)(r / 4 + 1);
+                for (int i = 0; i < 4; ++i) c.v[i] += ks[(s + i) % 5];
+                c.v[3] += s;
+            }
         }
         return c;
     }
@@ -147,17 +174,24 @@ struct RNGState {
 
 namespace detail {
 template <typename RNG>
+constexpr int32_t rng_tag() {
+    static_assert(std::is_same<RNG, r123::Philox4x32>::value || std::is_same<RNG, r123::Threefry4x32>::value,
+                  "the device draws r123::Philox4x32 and r123::Threefry4x32");
+    return std::is_same<RNG, r123::Threefry4x32>::value ? RBH_RNG_THREEFRY4X32 : RBH_RNG_PHILOX4X32;
+}
+template <typename RNG>
 inline rbh_state c_state(const RNGState<RNG> &s) {
-    rbh_state o;
+    rbh_state o{};
     std::memcpy(o.counter, s.counter.v, sizeof o.counter);
-    std::memcpy(o.key, s.key.v, sizeof o.key);
+    std::memcpy(o.key, s.key.v, sizeof s.key.v);   // (Philox: key words 2-3 stay zero)
+    o.rng = rng_tag<RNG>();
     return o;
 }
 template <typename RNG>
 inline RNGState<RNG> from_c(const rbh_state &s) {
     RNGState<RNG> o;
     std::memcpy(o.counter.v, s.counter, sizeof s.counter);
-    std::memcpy(o.key.v, s.key, sizeof s.key);
+    std::memcpy(o.key.v, s.key, sizeof o.key.v);
     return o;
 }
 }  // namespace detail

@@ -31,10 +31,16 @@ extern "C" {
 #define RBH_ERR_HIP 2       /* HIP runtime / launch failure */
 #define RBH_ERR_SYMMETRY 3  /* util::require_symmetric failed (util.hh:165-188) */
 
-/* RNGState<r123::Philox4x32> (base.hh:161-232): 128-bit counter (little-endian u32 words) + key. */
+/* RNGState<RNG> (base.hh:161-232): 128-bit counter (little-endian u32 words) + key, and which
+ * Random123 generator RNG is (ABI 4): rng 0 = r123::Philox4x32 (Philox4x32-10, key[0..1]; key[2..3]
+ * ignored), 1 = r123::Threefry4x32 (Threefry4x32-20, key[0..3]). */
+#define RBH_RNG_PHILOX4X32 0
+#define RBH_RNG_THREEFRY4X32 1
 typedef struct rbh_state {
     uint32_t counter[4];
-    uint32_t key[2];
+    uint32_t key[4];
+    int32_t rng;
+    int32_t reserved;   /* 0 */
 } rbh_state;
 
 /* DenseDist (dense_skops.hh:222-294). */

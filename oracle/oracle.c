@@ -39,6 +39,45 @@ void rbo_philox4x32(const uint32_t ctr[4], const uint32_t key[2], int rounds, ui
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
+/* ------------------------------------------------------------------------------------------ */
+/* Random123 Threefry4x32-R (threefry.h; RandBLAS's RNGState<r123::Threefry4x32>, base.hh:159): */
+/* key schedule ks[4] = 0x1BD11BDA ^ k0 ^ k1 ^ k2 ^ k3; the key added before round 0 and after   */
+/* every 4th round (s-th injection: x_i += ks[(s + i) % 5], x3 += s); even rounds mix (x0, x1)   */
+/* and (x2, x3), odd rounds (x0, x3) and (x2, x1), rotations R_32x4[r % 8].                     */
+/* ------------------------------------------------------------------------------------------ */
+static inline uint32_t rotl32(uint32_t x, unsigned r) { return (x << r) | (x >> (32 - r)); }
+void rbo_threefry4x32(const uint32_t ctr[4], const uint32_t key[4], int rounds, uint32_t out[4]) {
+    static const unsigned R[8][2] = {{10, 26}, {11, 21}, {13, 27}, {23, 5}, {6, 20}, {17, 11}, {25, 10}, {18, 20}};
+    uint32_t ks[5], x[4];
+    ks[4] = 0x1BD11BDAu;
+    for (int i = 0; i < 4; ++i) { ks[i] = key[i]; x[i] = ctr[i] + key[i]; ks[4] ^= key[i]; }
+    for (int r = 0; r < rounds; ++r) {
+        const unsigned *rc = R[r % 8];
+        if (r % 2 == 0) {
+            x[0] += x[1]; x[1] = rotl32(x[1], rc[0]) ^ x[0];
+            x[2] += x[3]; x[3] = rotl32(x[3], rc[1]) ^ x[2];
+        } else {
+            x[0] += x[3]; x[3] = rotl32(x[3], rc[0]) ^ x[0];
+            x[2] += x[1]; x[1] = rotl32(x[1], rc[1]) ^ x[2];
+        }
+        if (r % 4 == 3) {
+            const uint32_t sI = (uint32_t)((r + 1) / 4);
+            for (int i = 0; i < 4; ++i) x[i] += ks[(sI + i) % 5];
+            x[3] += sI;
+        }
+    }
+    for (int i = 0; i < 4; ++i) out[i] = x[i];
+}
+
+/* The counter-based generator of the operators being restated: 0 Philox4x32-10 (key[0..1]), 1
+ * Threefry4x32-20 (key[0..3]); rbo_set_rng selects it (RNGState<RNG>'s template parameter). */
+static int g_rng = 0;
+void rbo_set_rng(int rng) { g_rng = rng; }
+void rbo_cbrng(const uint32_t ctr[4], const uint32_t key[4], uint32_t out[4]) {
+    if (g_rng == 1) rbo_threefry4x32(ctr, key, 20, out);
+    else rbo_philox4x32(ctr, key, 10, out);
+}
+
 /* ctr_type::incr(u64): 128-bit little-endian add with carry (test_r123.cc:679-766 pins it). */
 void rbo_ctr_incr(uint32_t c[4], uint64_t inc) {
     uint64_t lo = (uint64_t)c[0] + (uint32_t)inc;
@@ -74,9 +113,9 @@ static inline void boxmuller_f(uint32_t u0, uint32_t u1, float *x, float *y) {
 }
 
 /* r123ext::boxmul::generate / r123ext::uneg11::generate (random_gen.hh:96-173). */
-void rbo_generate4(char family, const uint32_t ctr[4], const uint32_t key[2], float out[4]) {
+void rbo_generate4(char family, const uint32_t ctr[4], const uint32_t key[4], float out[4]) {
     uint32_t w[4];
-    rbo_philox4x32(ctr, key, 10, w);
+    rbo_cbrng(ctr, key, w);
     if (family == 'G') {
         boxmuller_f(w[0], w[1], &out[0], &out[1]);
         boxmuller_f(w[2], w[3], &out[2], &out[3]);

@@ -44,7 +44,9 @@ RBH_OK, RBH_ERR_REQUIRE, RBH_ERR_HIP, RBH_ERR_SYMMETRY = 0, 1, 2, 3
 
 
 class RNGStateC(ctypes.Structure):
-    _fields_ = [("counter", ctypes.c_uint32 * 4), ("key", ctypes.c_uint32 * 2)]
+    # rbh_state (include/randblas_hip.h): key words 2-3 are Threefry4x32's, rng RBH_RNG_*
+    _fields_ = [("counter", ctypes.c_uint32 * 4), ("key", ctypes.c_uint32 * 4), ("rng", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
 
 
 class DenseDistC(ctypes.Structure):
@@ -161,13 +163,26 @@ Layout_ColMajor, Layout_RowMajor = "C", "R"
 Op_NoTrans, Op_Trans = "N", "T"
 
 
+RNGS = {"philox": 0, "threefry": 1}   # RBH_RNG_PHILOX4X32, RBH_RNG_THREEFRY4X32
+
+
 @dataclass
 class RNGState:
-    """RNGState<r123::Philox4x32> (RandBLAS/base.hh:161-232). RNGState(k): counter 0, key {k, 0}."""
+    """RNGState<RNG> (RandBLAS/base.hh:153-232). RNGState(k): counter 0, key {k, 0} -- rng "philox"
+    (r123::Philox4x32, the reference's default, a 2-word key) or "threefry" (r123::Threefry4x32,
+    key {k, key_hi, key_ext[0], key_ext[1]})."""
 
     key: int = 0
     counter: tuple = (0, 0, 0, 0)
     key_hi: int = 0
+    rng: str = "philox"
+    key_ext: tuple = (0, 0)
+
+    def __post_init__(self):
+        if self.rng not in RNGS:
+            raise ValueError(f"rng must be one of {sorted(RNGS)}, not {self.rng!r}")
+        if self.rng == "philox" and any(int(w) & 0xFFFFFFFF for w in self.key_ext):
+            raise ValueError("Philox4x32 has a 2-word key: key_ext must be zero")
 
     def c(self) -> RNGStateC:
         s = RNGStateC()
@@ -175,11 +190,16 @@ class RNGState:
             s.counter[i] = int(self.counter[i]) & 0xFFFFFFFF
         s.key[0] = int(self.key) & 0xFFFFFFFF
         s.key[1] = int(self.key_hi) & 0xFFFFFFFF
+        s.key[2] = int(self.key_ext[0]) & 0xFFFFFFFF
+        s.key[3] = int(self.key_ext[1]) & 0xFFFFFFFF
+        s.rng = RNGS[self.rng]
         return s
 
     @staticmethod
     def from_c(s: RNGStateC) -> "RNGState":
-        return RNGState(key=s.key[0], counter=tuple(s.counter), key_hi=s.key[1])
+        name = {v: k for k, v in RNGS.items()}[s.rng]
+        return RNGState(key=s.key[0], counter=tuple(s.counter), key_hi=s.key[1], rng=name,
+                        key_ext=(s.key[2], s.key[3]))
 
 
 @dataclass

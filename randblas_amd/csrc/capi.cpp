@@ -352,6 +352,7 @@ void make_gen(GenOperand &g, const rbh_dense_dist *D, const rbh_state *seed, int
     const int64_t L = major_axis_length(D);
     memcpy(g.ctr, seed->counter, sizeof g.ctr);
     memcpy(g.key, seed->key, sizeof g.key);
+    g.rng = seed->rng == RBH_RNG_THREEFRY4X32 ? rb::RNG_THREEFRY : rb::RNG_PHILOX;
     g.stride = (uint64_t)((L + 3) / 4);
     g.pr0 = nat_row ? ro : co;
     g.pc0 = nat_row ? co : ro;
@@ -441,6 +442,7 @@ int lskge3(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, T a
     }
     if (!S_buff) {
         RBH_REQUIRE(seed != nullptr);
+        RBH_REQUIRE(seed->rng == RBH_RNG_PHILOX4X32 || seed->rng == RBH_RNG_THREEFRY4X32);
         RBH_REQUIRE(D->family != 'B');
         RBH_REQUIRE(D->major_axis != 'U');
     } else {
@@ -530,6 +532,7 @@ int rskge3(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, T a
     }
     if (!S_buff) {
         RBH_REQUIRE(seed != nullptr);
+        RBH_REQUIRE(seed->rng == RBH_RNG_PHILOX4X32 || seed->rng == RBH_RNG_THREEFRY4X32);
         RBH_REQUIRE(D->family != 'B');
         RBH_REQUIRE(D->major_axis != 'U');
     } else {
@@ -616,6 +619,7 @@ template <typename T>
 int fill_dense(char layout, const rbh_dense_dist *D, int64_t n_rows, int64_t n_cols, int64_t ro_s, int64_t co_s,
                T *buff, const rbh_state *seed, rbh_state *next_state, void *stream) {
     RBH_REQUIRE(D != nullptr && seed != nullptr);
+    RBH_REQUIRE(seed->rng == RBH_RNG_PHILOX4X32 || seed->rng == RBH_RNG_THREEFRY4X32);
     RBH_REQUIRE(layout == 'C' || layout == 'R');
     RBH_REQUIRE(n_rows >= 0 && n_cols >= 0 && ro_s >= 0 && co_s >= 0);
     RBH_REQUIRE(D->n_rows >= n_rows + ro_s);
@@ -628,6 +632,7 @@ int fill_dense(char layout, const rbh_dense_dist *D, int64_t n_rows, int64_t n_c
     GenOperand g{};
     memcpy(g.ctr, seed->counter, sizeof g.ctr);
     memcpy(g.key, seed->key, sizeof g.key);
+    g.rng = seed->rng == RBH_RNG_THREEFRY4X32 ? rb::RNG_THREEFRY : rb::RNG_PHILOX;
     g.stride = (uint64_t)((L + 3) / 4);
     g.family = D->family == 'U' ? rb::UNIFORM : rb::GAUSSIAN;
     g.scale = (double)(T)std::sqrt(3.0);
@@ -695,6 +700,7 @@ SparseGen make_sparse_gen(const rbh_sparse_dist *D, const rbh_state *seed) {
     g.major_axis = D->major_axis;
     memcpy(g.ctr, seed->counter, sizeof g.ctr);
     memcpy(g.key, seed->key, sizeof g.key);
+    g.rng = seed->rng == RBH_RNG_THREEFRY4X32 ? rb::RNG_THREEFRY : rb::RNG_PHILOX;
     return g;
 }
 
@@ -716,6 +722,7 @@ int fill_sparse(const rbh_sparse_dist *D, const rbh_state *seed, int64_t *rows, 
     int rc = check_sparse_dist(D);
     if (rc) return rc;
     RBH_REQUIRE(seed != nullptr && rows != nullptr && cols != nullptr);
+    RBH_REQUIRE(seed->rng == RBH_RNG_PHILOX4X32 || seed->rng == RBH_RNG_THREEFRY4X32);
     const int64_t nnz = sparse_nnz(D);
     hipStream_t s = (hipStream_t)stream;
     Stager st(s);
@@ -762,6 +769,7 @@ int sparse_common(SparseApply &p, const rbh_sparse_dist *D, const rbh_state *see
     p.C = dB;
     if (!rows) {   // sample the operator on the device, inside the apply
         RBH_REQUIRE(seed != nullptr);
+        RBH_REQUIRE(seed->rng == RBH_RNG_PHILOX4X32 || seed->rng == RBH_RNG_THREEFRY4X32);
         RBH_HIP(run_sparse_sampled_t<T>(p, make_sparse_gen(D, seed), sparse_nnz(D), s));
     } else {
         RBH_REQUIRE(cols != nullptr && vals != nullptr && nnz >= 0);
@@ -900,6 +908,7 @@ int submat_dense(Stager &st, const rbh_dense_dist *D, const rbh_state *seed, con
         return RBH_OK;
     }
     RBH_REQUIRE(seed != nullptr);
+    RBH_REQUIRE(seed->rng == RBH_RNG_PHILOX4X32 || seed->rng == RBH_RNG_THREEFRY4X32);
     RBH_REQUIRE(D->family != 'B');
     RBH_REQUIRE(D->major_axis != 'U');
     RBH_HIP(ws_alloc(ws, sizeof(T) * (size_t)std::max<int64_t>(rs * cs, 1), s));
@@ -907,6 +916,7 @@ int submat_dense(Stager &st, const rbh_dense_dist *D, const rbh_state *seed, con
     GenOperand g{};
     memcpy(g.ctr, seed->counter, sizeof g.ctr);
     memcpy(g.key, seed->key, sizeof g.key);
+    g.rng = seed->rng == RBH_RNG_THREEFRY4X32 ? rb::RNG_THREEFRY : rb::RNG_PHILOX;
     g.stride = (uint64_t)((major_axis_length(D) + 3) / 4);
     g.family = D->family == 'U' ? rb::UNIFORM : rb::GAUSSIAN;
     g.scale = (double)(T)std::sqrt(3.0);
@@ -1304,6 +1314,7 @@ int check_sksy(char layout, char side, int64_t d, int64_t n, const rbh_dense_dis
     else RBH_REQUIRE(ldb >= bc);
     if (!S_buff) {
         RBH_REQUIRE(seed != nullptr);
+        RBH_REQUIRE(seed->rng == RBH_RNG_PHILOX4X32 || seed->rng == RBH_RNG_THREEFRY4X32);
         RBH_REQUIRE(D->family != 'B');
         RBH_REQUIRE(D->major_axis != 'U');
     } else {
@@ -1442,7 +1453,7 @@ int dense_plan(bool left, char layout, char opS, char opA, int64_t M1, int64_t M
 // =============================================================================================
 extern "C" {
 
-int rbh_abi_version(void) { return 3; }
+int rbh_abi_version(void) { return 4; }
 
 int rbh_release_workspaces_ex(void *stream, int all_streams) {
     const hipError_t e = ws_release((hipStream_t)stream, all_streams != 0);

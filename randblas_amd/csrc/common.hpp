@@ -26,7 +26,9 @@ enum OpKind : int {
 // the layout map of :494-503).
 struct GenOperand {
     uint32_t ctr[4];
-    uint32_t key[2];
+    uint32_t key[4];     // Philox reads key[0..1]
+    int rng;             // rb::RNG_PHILOX (every GEMM kernel) or rb::RNG_THREEFRY (drawn by fill_dense / gemv
+                         // only: launch_gemm materialises a Threefry window first)
     uint64_t stride;     // counters per natural row = ceil(L / 4), L = major-axis length
     int64_t pr0, pc0;    // natural coordinates of operand element (0, 0)
     int family;          // rb::GAUSSIAN / rb::UNIFORM

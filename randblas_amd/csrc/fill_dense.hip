@@ -37,7 +37,7 @@ __global__ __launch_bounds__(FD_NT) void fill_dense_rows_kernel(const GenOperand
     for (int64_t r = blockIdx.y; r < n_rows_; r += gridDim.y) {
         uint32_t ctr[4];
         rb::ctr_add(g.ctr, (uint64_t)(g.pr0 + r) * g.stride + (uint64_t)q, ctr);
-        const rb::u32x4 w = rb::philox4x32_uk<10>(ctr[0], ctr[1], ctr[2], ctr[3], g.key[0], g.key[1]);
+        const rb::u32x4 w = rb::cbrng(g.rng, ctr, g.key);
         float sm[4];
         rb::sample4<FAMILY>(w, sm, tab);
         v4_t v;
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(FD_NT) void fill_dense_cols_kernel(const GenOperand
         const int64_t q = qa + qi;
         uint32_t ctr[4];
         rb::ctr_add(g.ctr, rowc + (uint64_t)q, ctr);
-        const rb::u32x4 w = rb::philox4x32_uk<10>(ctr[0], ctr[1], ctr[2], ctr[3], g.key[0], g.key[1]);
+        const rb::u32x4 w = rb::cbrng(g.rng, ctr, g.key);
         float sm[4];
         rb::sample4<FAMILY>(w, sm, tab);
 #pragma unroll

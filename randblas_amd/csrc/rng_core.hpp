@@ -102,6 +102,49 @@ RB_HD u32x4 philox4x32_uk(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, ui
 #endif
 }
 
+// Random123 Threefry4x32-R (threefry.h), RandBLAS's other counter-based generator
+// (RNGState<r123::Threefry4x32>, base.hh:159; Random123's default R = 20): key schedule
+// ks[4] = 0x1BD11BDA ^ k0 ^ k1 ^ k2 ^ k3, the key added before round 0 and after every 4th round
+// (injection s: x_i += ks[(s + i) % 5], x3 += s); even rounds mix (x0, x1), (x2, x3), odd rounds
+// (x0, x3), (x2, x1), with the rotations R_32x4[r % 8]. Pinned by the reference's KAT rows
+// (tests/golden/threefry4x32_kat.txt).
+RB_HD uint32_t rotl32(uint32_t x, unsigned r) { return (x << r) | (x >> (32u - r)); }
+template <int R = 20>
+RB_HD u32x4 threefry4x32(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1, uint32_t k2,
+                         uint32_t k3) {
+    const uint32_t ks[5] = {k0, k1, k2, k3, 0x1BD11BDAu ^ k0 ^ k1 ^ k2 ^ k3};
+    uint32_t x0 = c0 + k0, x1 = c1 + k1, x2 = c2 + k2, x3 = c3 + k3;
+    constexpr unsigned ROT[8][2] = {{10, 26}, {11, 21}, {13, 27}, {23, 5}, {6, 20}, {17, 11}, {25, 10}, {18, 20}};
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int r = 0; r < R; ++r) {
+        if (r % 2 == 0) {
+            x0 += x1; x1 = rotl32(x1, ROT[r % 8][0]) ^ x0;
+            x2 += x3; x3 = rotl32(x3, ROT[r % 8][1]) ^ x2;
+        } else {
+            x0 += x3; x3 = rotl32(x3, ROT[r % 8][0]) ^ x0;
+            x2 += x1; x1 = rotl32(x1, ROT[r % 8][1]) ^ x2;
+        }
+        if (r % 4 == 3) {
+            const uint32_t s = (uint32_t)((r + 1) / 4);
+            x0 += ks[s % 5]; x1 += ks[(s + 1) % 5]; x2 += ks[(s + 2) % 5]; x3 += ks[(s + 3) % 5] + s;
+        }
+    }
+    u32x4 out = {{x0, x1, x2, x3}};
+    return out;
+}
+
+// The operators' generator (RNGState<RNG>): rng 0 Philox4x32-10 (key[0..1]), 1 Threefry4x32-20
+// (key[0..3]). The streamed / tiled GEMM kernels call Philox directly; a Threefry operator reaches
+// them only as a window drawn by this one (fill_dense) into a workspace.
+constexpr int RNG_PHILOX = 0, RNG_THREEFRY = 1;
+struct CbKey { uint32_t k[4]; int rng; };   // a generator's key and kind, as one kernel argument
+RB_HD u32x4 cbrng(int rng, const uint32_t c[4], const uint32_t k[4]) {
+    if (rng == RNG_THREEFRY) return threefry4x32<20>(c[0], c[1], c[2], c[3], k[0], k[1], k[2], k[3]);
+    return philox4x32_uk<10>(c[0], c[1], c[2], c[3], k[0], k[1]);
+}
+
 // 128-bit counter = base (4 x u32, little-endian words) + off (u64), carries across words.
 RB_HD void ctr_add(const uint32_t base[4], uint64_t off, uint32_t out[4]) {
     uint64_t lo = (uint64_t)base[0] + (uint32_t)off;

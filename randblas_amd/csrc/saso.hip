@@ -47,7 +47,7 @@ constexpr int SP_KC = 128;        // contracted indices per chunk (LDS panel dep
 // 1. fill_sparse
 // ------------------------------------------------------------------------------------------
 template <typename T, int MAXNNZ>
-__global__ void fill_sparse_kernel(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
+__global__ void fill_sparse_kernel(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, const rb::CbKey key,
                                    int64_t vec_nnz, int64_t dim_major, int64_t dim_minor, int64_t *idx_major,
                                    int64_t *idx_minor, T *vals) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -60,7 +60,7 @@ __global__ void fill_sparse_kernel(uint32_t c0, uint32_t c1, uint32_t c2, uint32
     for (int64_t j = 0; j < vec_nnz; ++j) {
         uint32_t ctr[4];
         rb::ctr_add(base, (uint64_t)(offset + j), ctr);
-        const rb::u32x4 rv = rb::philox4x32<10>(ctr[0], ctr[1], ctr[2], ctr[3], k0, k1);
+        const rb::u32x4 rv = rb::cbrng(key.rng, ctr, key.k);
         const int64_t ell = j + (int64_t)(rv.v[0] % (uint64_t)(dim_major - j));
         // current values work[j], work[ell]
         int tj = -1, tl = -1;
@@ -106,7 +106,7 @@ __device__ __forceinline__ bool sp_locate_rc(int64_t r, int64_t c, const SparseA
 
 template <typename T, bool MARK>
 __global__ __launch_bounds__(64) void fill_sparse_small_kernel(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                                              uint32_t k0, uint32_t k1, int vec_nnz,
+                                                              const rb::CbKey key, int vec_nnz,
                                                               uint32_t dim_major, int64_t dim_minor, int maj_is_row,
                                                               int64_t *idx_major, int64_t *idx_minor, T *vals,
                                                               SparseApply p, uint32_t *mask) {
@@ -120,7 +120,7 @@ __global__ __launch_bounds__(64) void fill_sparse_small_kernel(uint32_t c0, uint
 #pragma unroll
     for (int j = 0; j < SF_NZ; ++j) {
         if (j >= vec_nnz) break;
-        const rb::u32x4 rv = rb::philox4x32<10>(ctr[0], ctr[1], ctr[2], ctr[3], k0, k1);
+        const rb::u32x4 rv = rb::cbrng(key.rng, ctr, key.k);
         const uint32_t ell = (uint32_t)j + rv.v[0] % (dim_major - (uint32_t)j);
         uint32_t wj = (uint32_t)j, wl = ell;
 #pragma unroll
@@ -158,14 +158,15 @@ static hipError_t launch_fill_sparse_t(const SparseGen &g, int64_t *rows, int64_
     if (g.major_axis == 'S') { dim_major = short_ax; dim_minor = long_ax; imaj = short_idx; imin = long_idx; }
     else { dim_major = long_ax; dim_minor = short_ax; imaj = long_idx; imin = short_idx; }
     if (dim_minor <= 0) return hipSuccess;
+    const rb::CbKey gk{{g.key[0], g.key[1], g.key[2], g.key[3]}, g.rng};
     if (g.vec_nnz <= SF_NZ && dim_major < ((int64_t)1 << 31)) {
         const unsigned b64 = (unsigned)((dim_minor + 63) / 64);
         const SparseApply none{};
         if (mask) hipLaunchKernelGGL((fill_sparse_small_kernel<T, true>), dim3(b64), dim3(64), 0, s, g.ctr[0], g.ctr[1],
-                                    g.ctr[2], g.ctr[3], g.key[0], g.key[1], (int)g.vec_nnz, (uint32_t)dim_major,
+                                    g.ctr[2], g.ctr[3], gk, (int)g.vec_nnz, (uint32_t)dim_major,
                                     dim_minor, (int)(g.major_axis == 'S' ? is_wide : !is_wide), imaj, imin, vals, *mark_p, mask);
         else hipLaunchKernelGGL((fill_sparse_small_kernel<T, false>), dim3(b64), dim3(64), 0, s, g.ctr[0], g.ctr[1],
-                                g.ctr[2], g.ctr[3], g.key[0], g.key[1], (int)g.vec_nnz, (uint32_t)dim_major,
+                                g.ctr[2], g.ctr[3], gk, (int)g.vec_nnz, (uint32_t)dim_major,
                                 dim_minor, (int)(g.major_axis == 'S' ? is_wide : !is_wide), imaj, imin, vals, none, (uint32_t *)nullptr);
         return hipGetLastError();
     }
@@ -173,7 +174,7 @@ static hipError_t launch_fill_sparse_t(const SparseGen &g, int64_t *rows, int64_
     const unsigned blocks = (unsigned)((dim_minor + 255) / 256);
 #define RBH_FS(MAXN)                                                                                        \
     hipLaunchKernelGGL((fill_sparse_kernel<T, MAXN>), dim3(blocks), dim3(256), 0, s, g.ctr[0], g.ctr[1],   \
-                       g.ctr[2], g.ctr[3], g.key[0], g.key[1], g.vec_nnz, dim_major, dim_minor, imaj, imin, vals)
+                       g.ctr[2], g.ctr[3], gk, g.vec_nnz, dim_major, dim_minor, imaj, imin, vals)
     if (g.vec_nnz <= 8) RBH_FS(8);
     else if (g.vec_nnz <= 32) RBH_FS(32);
     else if (g.vec_nnz <= 128) RBH_FS(128);

@@ -9,7 +9,8 @@ struct SparseGen {
     int64_t n_rows, n_cols, vec_nnz;
     char major_axis;   // 'S' (SASO) or 'L' (LASO)
     uint32_t ctr[4];
-    uint32_t key[2];
+    uint32_t key[4];
+    int rng;   // rb::RNG_PHILOX / rb::RNG_THREEFRY (RNGState<RNG>)
 };
 
 // Canonical sparse apply: C (M x N, element (i,j) at C[i*crs + j*ccs]) =

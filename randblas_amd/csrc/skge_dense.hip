@@ -2219,6 +2219,26 @@ static bool tri_ok(const GemmProblem &p) {
 // counter along k from a Philox quad (GEN_OK, every MajorAxis::Long operator) and K % 16 == 0; full
 // storage also needs 16-B aligned rows. Otherwise hipErrorNotSupported, and the caller expands
 // the triangle (launch_symmetrize) and runs the plain kernels.
+// A Threefry operator (RNGState<r123::Threefry4x32>, base.hh:153-161) in a GEMM problem: the GEMM
+// kernels draw Philox4x32 only (the generator sits on their critical issue path), so such a window
+// is drawn by fill_dense into a workspace first, element (o, k) at buf[o K + k], and the problem
+// runs with it as a memory operand -- the reference's fill_dense + gemm shape (skge.hh:173-215). The
+// gemv kernel (sketch_vector) draws either generator itself.
+static bool threefry_gen(const GemmProblem &p) {
+    return (p.xkind != MEM && p.xg.rng == rb::RNG_THREEFRY) || (p.ykind != MEM && p.yg.rng == rb::RNG_THREEFRY);
+}
+template <typename T>
+static void threefry_as_mem(GemmProblem &q, bool gx, const void *buf) {
+    int &kind = gx ? q.xkind : q.ykind;
+    int &mode = gx ? q.xmode : q.ymode;
+    MemOperand &m = gx ? q.xm : q.ym;
+    kind = MEM;
+    m.ptr = buf;
+    m.so = q.K;
+    m.sk = 1;
+    mode = (q.K % (16 / (int64_t)sizeof(T))) == 0 ? 2 : 1;   // (workspaces are 256-B aligned)
+}
+
 template <typename T>
 static hipError_t launch_gemm_tri(const GemmProblem &p, hipStream_t s) {
     if (!tri_ok<T>(p)) return hipErrorNotSupported;
@@ -2255,6 +2275,12 @@ static GemmPlan plan_gemm(const GemmProblem &p) {
     GemmPlan pl{PLAN_NONE, 1, 0, 0};
     if (p.M <= 0 || p.N <= 0) return pl;
     if (p.K <= 0 || p.alpha == 0.0) { pl.kernel = PLAN_SCALE; return pl; }
+    if (threefry_gen(p) && !gemv_ok(p)) {   // as launch_gemm_threefry: the window drawn first
+        GemmProblem q = p;
+        if (q.xkind != MEM && q.xg.rng == rb::RNG_THREEFRY) threefry_as_mem<T>(q, true, nullptr);
+        if (q.ykind != MEM && q.yg.rng == rb::RNG_THREEFRY) threefry_as_mem<T>(q, false, nullptr);
+        return plan_gemm<T>(q);
+    }
     if (!p.tri && gemv_ok(p)) {   // one vector operand: sketch_vector (skve.hip)
         pl.kernel = PLAN_GEMV;
         pl.splitk = gemv_split(p);
@@ -2320,7 +2346,44 @@ GemmPlan plan_gemm_f64(const GemmProblem &p) { return plan_gemm<double>(p); }
 GemmPlan plan_gemm_f32(const GemmProblem &p) { return plan_gemm<float>(p); }
 
 template <typename T>
+static hipError_t launch_gemm(const GemmProblem &p, hipStream_t s);
+
+template <typename T>
+static hipError_t launch_gemm_threefry(const GemmProblem &p, hipStream_t s) {
+    GemmProblem q = p;
+    void *bufs[2] = {nullptr, nullptr};
+    hipError_t e = hipSuccess;
+    for (int side = 0; side < 2 && e == hipSuccess; ++side) {
+        const bool gx = side == 0;
+        const int kind = gx ? p.xkind : p.ykind;
+        const GenOperand &g = gx ? p.xg : p.yg;
+        if (kind == MEM || g.rng != rb::RNG_THREEFRY) continue;
+        const int64_t nO = gx ? p.M : p.N;
+        e = ws_alloc(&bufs[side], sizeof(T) * (size_t)nO * (size_t)p.K, s);
+        if (e != hipSuccess) break;
+        // GEN_OK: natural rows o, columns k (row-major window); GEN_OO: natural rows k, stored transposed
+        if (sizeof(T) == 8)
+            e = kind == GEN_OK ? launch_fill_dense_f64(g, nO, p.K, 0, (double *)bufs[side], s)
+                               : launch_fill_dense_f64(g, p.K, nO, 1, (double *)bufs[side], s);
+        else
+            e = kind == GEN_OK ? launch_fill_dense_f32(g, nO, p.K, 0, (float *)bufs[side], s)
+                               : launch_fill_dense_f32(g, p.K, nO, 1, (float *)bufs[side], s);
+        threefry_as_mem<T>(q, gx, bufs[side]);
+    }
+    if (e == hipSuccess) e = launch_gemm<T>(q, s);
+    for (void *b : bufs)
+        if (b) {
+            const hipError_t e2 = ws_free(b, s);
+            if (e == hipSuccess) e = e2;
+        }
+    return e;
+}
+
+template <typename T>
 static hipError_t launch_gemm(const GemmProblem &p, hipStream_t s) {
+    // (a one-triangle read needs a generated operand: the caller symmetrizes and calls again)
+    if (p.tri && threefry_gen(p)) return hipErrorNotSupported;
+    if (threefry_gen(p) && !gemv_ok(p)) return launch_gemm_threefry<T>(p, s);
     if (p.tri) return launch_gemm_tri<T>(p, s);
     const bool unif = (p.xkind != MEM ? p.xg.family : p.yg.family) == rb::UNIFORM;
     const int kernel = plan_gemm<T>(p).kernel;

@@ -27,7 +27,7 @@ template <typename T, int FAMILY>
 __device__ __forceinline__ void ve_call(const GenOperand &g, uint64_t off, T out[4]) {
     uint32_t c[4];
     rb::ctr_add(g.ctr, off, c);
-    const rb::u32x4 w = rb::philox4x32_uk<10>(c[0], c[1], c[2], c[3], g.key[0], g.key[1]);
+    const rb::u32x4 w = rb::cbrng(g.rng, c, g.key);   // (Philox or Threefry: RNGState<RNG>)
     float s[4];
     rb::sample4<FAMILY>(w, s);
 #pragma unroll

@@ -603,6 +603,56 @@ static void filled_operator_fast_path() {
     (void)hipFree(dr); (void)hipFree(dc); (void)hipFree(dv); (void)hipFree(dA); (void)hipFree(dB);
 }
 
+// RNGState<r123::Threefry4x32> (base.hh:153-161): the header's host generator on the reference's
+// known-answer row (test/test_basic_rng/r123_kat_vectors.txt), and dense / sparse operators drawn by
+// the device's Threefry generator
+static void threefry_operators() {
+    using TF = r123::Threefry4x32;
+    const TF::ctr_type c = {{0x243f6a88u, 0x85a308d3u, 0x13198a2eu, 0x03707344u}};
+    const TF::key_type k = {{0xa4093822u, 0x299f31d0u, 0x082efa98u, 0xec4e6c89u}};
+    const TF::ctr_type r = TF()(c, k);
+    CHECK(r[0] == 0x59cd1dbbu && r[1] == 0xb8879579u && r[2] == 0x86b5d00cu && r[3] == 0xac8b6d84u);
+
+    const int64_t d = 20, m = 150, n = 7;
+    RandBLAS::DenseDist D(d, m);
+    RandBLAS::DenseSkOp<double, TF> S(D, RandBLAS::RNGState<TF>(3));
+    auto A = random_matrix<double>(m, n, 11);
+    std::vector<double> B(d * n, 0.0);
+    RandBLAS::sketch_general(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, m, 1.0, S, A.data(), m, 0.0, B.data(), d);
+    std::vector<double> Se(d * m), Sp(d * m);
+    const RandBLAS::RNGState<TF> next = RandBLAS::fill_dense(Layout::ColMajor, D, d, m, 0, 0, Se.data(), S.seed_state);
+    RandBLAS::fill_dense(Layout::ColMajor, D, d, m, 0, 0, Sp.data(), RandBLAS::RNGState<>(3));
+    int64_t differ = 0;
+    for (int64_t e = 0; e < d * m; ++e) differ += Se[e] != Sp[e];
+    CHECK(differ > d * m / 2);   // not the Philox operator of the same key
+    CHECK(next.key == S.seed_state.key && !(next.counter == S.seed_state.counter));
+    for (int64_t i = 0; i < d; ++i)
+        for (int64_t j = 0; j < n; ++j) {
+            double ex = 0, bound = 0;
+            for (int64_t q = 0; q < m; ++q) {
+                ex += Se[i + q * d] * A[q + j * m];
+                bound += std::fabs(Se[i + q * d] * A[q + j * m]);
+            }
+            CHECK(std::fabs(B[i + j * d] - ex) <= bound * m * 2 * std::numeric_limits<double>::epsilon());
+        }
+    CHECK(S.buff == nullptr);
+
+    // SASO: the lazily drawn operator and its filled arrays give the same bits
+    RandBLAS::SparseDist DS{d, m, 3};
+    RandBLAS::SparseSkOp<double, TF> Q(DS, RandBLAS::RNGState<TF>(9));
+    std::vector<double> C(d * n, 0.0), C2(d * n, 0.0);
+    RandBLAS::sketch_general(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, m, 1.0, Q, A.data(), m, 0.0, C.data(), d);
+    RandBLAS::SparseSkOp<double, TF> Q2(DS, RandBLAS::RNGState<TF>(9));
+    RandBLAS::fill_sparse(Q2);
+    RandBLAS::SparseSkOp<double> Qp(DS, 9);
+    RandBLAS::fill_sparse(Qp);
+    int64_t same = 0;
+    for (int64_t e = 0; e < Q2.nnz_count(); ++e) same += Q2.rows[e] == Qp.rows[e];
+    CHECK(same < Q2.nnz_count());
+    RandBLAS::sketch_general(Layout::ColMajor, Op::NoTrans, Op::NoTrans, d, n, m, 1.0, Q2, A.data(), m, 0.0, C2.data(), d);
+    for (int64_t e = 0; e < d * n; ++e) CHECK(C[e] == C2[e]);
+}
+
 int main() {
 #ifdef ONLY_SKSP   // diagnostics: the sketch_sparse checks alone
     try {
@@ -628,6 +678,7 @@ int main() {
     symmetric_one_triangle();
     namespaced_entry_points();
     filled_operator_fast_path();
+    threefry_operators();
     if (g_fail) {
         std::printf("%d checks FAILED\n", g_fail);
         return 1;

@@ -39,6 +39,8 @@ lib.rbo_generate4.argtypes = [c_char, u32p, u32p, ctypes.POINTER(ctypes.c_float)
 lib.rbo_dense_next_state.argtypes = [c_i64, c_i64, c_char, u32p, u32p]
 lib.rbo_sparse_next_state.argtypes = [c_i64, c_i64, c_i64, c_char, u32p, u32p]
 lib.rbo_set_threads.argtypes = [ctypes.c_int]
+lib.rbo_set_rng.argtypes = [ctypes.c_int]
+lib.rbo_threefry4x32.argtypes = [u32p, u32p, ctypes.c_int, u32p]
 for t, ct in (("d", ctypes.c_double), ("s", ctypes.c_float)):
     getattr(lib, f"rbo_fill_dense_{t}").argtypes = [c_char, c_i64, c_i64, c_char, c_char, c_i64, c_i64, c_i64, c_i64,
                                                     c_vp, u32p, u32p, u32p]
@@ -103,18 +105,31 @@ def ctr_incr(ctr, inc):
 
 def generate4(family, ctr, key):
     out = (ctypes.c_float * 4)()
-    lib.rbo_generate4(family.encode(), _u32(ctr), _u32(key), out)
+    lib.rbo_generate4(family.encode(), _u32(ctr), _u32(list(key) + [0] * (4 - len(key))), out)
     return np.array(list(out), dtype=np.float32)
 
 
-def seed_arrays(key=0, counter=(0, 0, 0, 0), key_hi=0):
-    return _u32(counter), _u32([key, key_hi])
+def seed_arrays(key=0, counter=(0, 0, 0, 0), key_hi=0, key_ext=(0, 0)):
+    """RNGState's counter and key arrays; keys are passed as 4 words (Philox reads the first two)."""
+    return _u32(counter), _u32([key, key_hi, key_ext[0], key_ext[1]])
+
+
+def set_rng(name):
+    """The operators' counter-based generator: "philox" (Philox4x32-10, the default) or "threefry"
+    (Threefry4x32-20), RNGState<RNG>'s template parameter (base.hh:159)."""
+    lib.rbo_set_rng({"philox": 0, "threefry": 1}[name])
+
+
+def threefry(ctr, key, rounds=20):
+    out = (ctypes.c_uint32 * 4)()
+    lib.rbo_threefry4x32(_u32(ctr), _u32(key), rounds, out)
+    return list(out)
 
 
 def fill_dense(layout, D_rows, D_cols, family, major_axis, n_rows, n_cols, ro_s, co_s, key=0, counter=(0, 0, 0, 0),
-               dtype=np.float64):
+               dtype=np.float64, key_hi=0, key_ext=(0, 0)):
     buf = np.zeros(n_rows * n_cols, dtype=dtype)
-    c, k = seed_arrays(key, counter)
+    c, k = seed_arrays(key, counter, key_hi, key_ext)
     nxt = (ctypes.c_uint32 * 4)()
     _check(getattr(lib, f"rbo_fill_dense_{_dt(dtype)}")(layout.encode(), D_rows, D_cols, family.encode(),
                                                          major_axis.encode(), n_rows, n_cols, ro_s, co_s,
@@ -138,12 +153,13 @@ def sparse_nnz(D_rows, D_cols, vec_nnz, major_axis):
     return vec_nnz * (max(D_rows, D_cols) if major_axis == "S" else min(D_rows, D_cols))
 
 
-def fill_sparse(D_rows, D_cols, vec_nnz, major_axis, key=0, counter=(0, 0, 0, 0), dtype=np.float64):
+def fill_sparse(D_rows, D_cols, vec_nnz, major_axis, key=0, counter=(0, 0, 0, 0), dtype=np.float64, key_hi=0,
+                key_ext=(0, 0)):
     nnz = sparse_nnz(D_rows, D_cols, vec_nnz, major_axis)
     rows = np.zeros(nnz, dtype=np.int64)
     cols = np.zeros(nnz, dtype=np.int64)
     vals = np.zeros(nnz, dtype=dtype)
-    c, k = seed_arrays(key, counter)
+    c, k = seed_arrays(key, counter, key_hi, key_ext)
     _check(getattr(lib, f"rbo_fill_sparse_{_dt(dtype)}")(D_rows, D_cols, vec_nnz, major_axis.encode(), c, k,
                                                           rows.ctypes.data, cols.ctypes.data, vals.ctypes.data))
     return rows, cols, vals

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert rb.abi_version() == 3
+    assert rb.abi_version() == 4
 
 
 @pytest.mark.parametrize("dims", [(10, 37), (37, 10), (64, 64), (5, 3), (1024, 16384)])
@@ -105,7 +105,7 @@ def test_argument_checks_fill_dense():
 
 
 def test_header_structs_match_ctypes():
-    assert ctypes.sizeof(rb.RNGStateC) == 24
+    assert ctypes.sizeof(rb.RNGStateC) == 40
     assert ctypes.sizeof(rb.DenseDistC) == 24
     assert ctypes.sizeof(rb.SparseDistC) == 32
     assert ctypes.sizeof(rb.OptionsC) == 16

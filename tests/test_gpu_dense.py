@@ -84,7 +84,7 @@ def _pos(layout, lds, ro, co):
 
 
 def check_left(cuda, layout, opS, opA, d, n, m, alpha, beta, SR, SC, ro, co, dtype, fam="G", maj="L",
-               explicit=False, skey=0, options=None):
+               explicit=False, skey=0, options=None, rng="philox"):
     rA, cA = (m, n) if opA == "N" else (n, m)
     A = O.random_matrix(rA, cA, 99, dtype)
     lda = rA if layout == "C" else cA
@@ -97,7 +97,7 @@ def check_left(cuda, layout, opS, opA, d, n, m, alpha, beta, SR, SC, ro, co, dty
     pos = _pos(layout, lds, ro, co)
     E = O.error_bound_left(layout, opS, opA, d, n, m, alpha, np.abs(S[pos:]).copy(), lds, A, lda, beta, B0, ldb, dtype)
     # device
-    Sop = rb.DenseSkOp(rb.DenseDist(SR, SC, fam, maj), rb.RNGState(key=skey))
+    Sop = rb.DenseSkOp(rb.DenseDist(SR, SC, fam, maj), rb.RNGState(key=skey, rng=rng))
     if explicit:
         Sop.buff = dev(S, cuda)
         Sop.buff_layout = layout
@@ -192,7 +192,7 @@ def test_lskge3_identity_probe(cuda):
 
 
 def check_right(cuda, layout, opA, opS, m, d, n, alpha, beta, SR, SC, ro, co, dtype, fam="G", maj="L",
-                explicit=False, skey=0, options=None):
+                explicit=False, skey=0, options=None, rng="philox"):
     rA, cA = (m, n) if opA == "N" else (n, m)
     A = O.random_matrix(rA, cA, 57, dtype)
     lda = rA if layout == "C" else cA
@@ -206,7 +206,7 @@ def check_right(cuda, layout, opA, opS, m, d, n, alpha, beta, SR, SC, ro, co, dt
     E = np.abs(B0).astype(dtype) if beta != 0 else np.zeros_like(B0)
     O.gemm(layout, opA, opS, m, d, n, abs(alpha) * n * 2 * eps, np.abs(A), lda, np.abs(S[pos:]).copy(), lds,
            abs(beta) * eps, E, ldb)
-    Sop = rb.DenseSkOp(rb.DenseDist(SR, SC, fam, maj), rb.RNGState(key=skey))
+    Sop = rb.DenseSkOp(rb.DenseDist(SR, SC, fam, maj), rb.RNGState(key=skey, rng=rng))
     if explicit:
         Sop.buff = dev(S, cuda)
         Sop.buff_layout = layout

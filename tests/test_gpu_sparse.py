@@ -53,7 +53,7 @@ def test_fill_sparse_bitwise(cuda, dims, vec_nnz, major, key):
 
 
 def check_left(cuda, layout, opS, opA, d, n, m, alpha, beta, SR, SC, vec, major, key, ro, co, dtype, given=False,
-               vals_fn=None):
+               vals_fn=None, rng="philox"):
     rA, cA = (m, n) if opA == "N" else (n, m)
     A = O.random_matrix(rA, cA, 99, dtype)
     lda = rA if layout == "C" else cA
@@ -64,7 +64,7 @@ def check_left(cuda, layout, opS, opA, d, n, m, alpha, beta, SR, SC, vec, major,
         vals = vals_fn(vals).astype(dtype)
     Bexp = B0.copy()
     O.left_spmm_coo(layout, opS, opA, d, n, m, alpha, SR, SC, rows, cols, vals, ro, co, A, lda, beta, Bexp, ldb)
-    S = rb.SparseSkOp(rb.SparseDist(SR, SC, vec, major), rb.RNGState(key=key))
+    S = rb.SparseSkOp(rb.SparseDist(SR, SC, vec, major), rb.RNGState(key=key, rng=rng))
     if given:   # user-provided COO arrays (SparseSkOp(dist, state, rows, cols, vals), sparse_skops.hh:268-291)
         perm = np.random.default_rng(5).permutation(len(rows))
         S.rows, S.cols, S.vals = dev(rows[perm], cuda), dev(cols[perm], cuda), dev(vals[perm], cuda)

@@ -34,6 +34,26 @@ def test_philox_kat(row):
     assert O.philox(ctr, key, rounds) == expected
 
 
+def threefry_rows():
+    rows = []
+    with open(os.path.join(ROOT, "tests", "golden", "threefry4x32_kat.txt")) as f:
+        for line in f:
+            if line.startswith("#") or not line.strip():
+                continue
+            p = line.split()
+            rows.append((int(p[1]), [int(x, 16) for x in p[2:6]], [int(x, 16) for x in p[6:10]],
+                         [int(x, 16) for x in p[10:14]]))
+    return rows
+
+
+@pytest.mark.parametrize("row", threefry_rows())
+def test_threefry_kat(row):
+    """Threefry4x32 (RNGState<r123::Threefry4x32>, base.hh:159) against the reference's known-answer
+    rows (r123_kat_vectors.txt:47-55): 13, 20 (Random123's default) and 72 rounds."""
+    rounds, ctr, key, expected = row
+    assert O.threefry(ctr, key, rounds) == expected
+
+
 def test_ctr_incr_semantics():
     # test_r123.cc:679-766
     i32max = 2**32 - 1

@@ -6,6 +6,9 @@ sketch_sparse (sksp.hh:147-194), one JSON line per shape (events around the libr
     every operator entry is drawn once and used once, so the bound is the draw rate. Reported as
     operator entries per second next to fill_dense of the same d x m window into HBM (the draw plus
     an 8-B store per entry: what materialising S first, the reference's fill_dense + gemv, costs).
+  * a Threefry operator (RNGState<r123::Threefry4x32>) in a dense sketch: its window is drawn by
+    fill_dense into a workspace and applied from there; timed beside the Philox operator of the same
+    shape (drawn inside the GEMM) and with the plan both report.
   * sketch_sparse B = S A (S d x m Gaussian, A m x n COO at a density): the library fills submat(S)
     on the device (sksp.hh:168-172) and applies A as the sparse operand; bytes = S written and read
     once + B written + A's COO arrays (24 B per entry), against 8 TB/s.
@@ -69,6 +72,19 @@ def sparse(d, m, n, dens):
                       "apply": rb.sparse_last_path()}), flush=True)
 
 
+def threefry_dense(d, m, n):
+    A = torch.randn(m * n, dtype=torch.float64, device=dev)
+    B = torch.empty(d * n, dtype=torch.float64, device=dev)
+    rec = {"path": "sketch_general_threefry", "d": d, "m": m, "n": n}
+    for rng in ("philox", "threefry"):
+        S = rb.DenseSkOp(rb.DenseDist(d, m), rb.RNGState(0, rng=rng))
+        t = timed(lambda: rb.sketch_general_left("C", "N", "N", d, n, m, 1.0, S, A, m, 0.0, B, d))
+        pl = rb.plan_left("C", "N", "N", d, n, m, S, A, m, d)
+        rec[rng] = {"ms": t, "tflops": 2 * d * m * n / (t * 1e-3) / 1e12, "plan": pl.kernel, "splitk": pl.splitk}
+    print(json.dumps(rec), flush=True)
+    del A, B
+
+
 def filld(d, m, layout):
     buf = torch.empty(d * m, dtype=torch.float64, device=dev)
     t = timed(lambda: rb.fill_dense(layout, rb.DenseDist(d, m), d, m, 0, 0, buf, rb.RNGState(0)))
@@ -79,6 +95,8 @@ def filld(d, m, layout):
 if __name__ == "__main__":
     for layout in ("R", "C"):
         filld(4096, 65536, layout)
+    for d, m, n in ((2048, 16384, 16384), (1024, 16384, 4096)):
+        threefry_dense(d, m, n)
     for d, m in ((1024, 16384), (2048, 65536), (4096, 262144)):
         vector(d, m)
     for d, m, n, dens in ((1024, 16384, 16384, 1e-3), (1024, 16384, 16384, 1e-2), (256, 65536, 8192, 1e-3)):
