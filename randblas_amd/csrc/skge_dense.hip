@@ -30,6 +30,9 @@
 namespace rbh {
 
 constexpr int BK = 16;
+// skge_stream_kernel's FAMILY for an operator read from memory instead of drawn (explicit buffers,
+// Threefry windows; launch_gemm_mat)
+constexpr int FAM_MAT = 2;
 // waves that load a materialised operator tile in the wide kernels (see skge_wide_kernel)
 // (measured, same box, both orders: f64 C2 8 waves 8.49-8.53 ms, 1 8.52-8.54, 2 8.57-8.59, 4 8.61-8.63;
 // f32 C4 4 waves 4.36 ms, 2 4.51-4.53, 1 and 8 4.65-4.67)
@@ -1196,6 +1199,9 @@ __global__ __launch_bounds__(512) void skge_wide32_kernel(const GemmProblem p) {
 // loads were in flight)
 template <int N>
 __device__ __forceinline__ void vm_wait_n() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+// (FAM_MAT, TRI 5: the asm-loaded values pass through one empty asm before they are read)
+template <typename V>
+__device__ __forceinline__ void vm_fence4(V &v) { asm volatile("" : "+v"(v)::"memory"); }
 template <typename T>
 __device__ __forceinline__ void vm_fence(T (&s)[2]) { asm volatile("" : "+v"(s[0]), "+v"(s[1])::"memory"); }
 template <typename T>
@@ -1490,8 +1496,103 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
         rb::ctr_add(gop.ctr, off, cbase);
     }
     const bool gtile_full = go0 + BG <= gnO;
+    // FAM_MAT: the operand is not drawn but read from memory (an explicit or pre-drawn operator: the
+    // memory descriptor on the generated side, rows contiguous along k for GEN_OK, along o for GEN_OO,
+    // 16-B aligned), each lane reading the 4 values its Philox call would have made, into the same LDS
+    // slots: the MFMAs see the same tile. A round's loads are issued as it starts and stored as it
+    // ends, so their latency hides under its steps. TRI 5 issues them as inline asm like its ring (the
+    // compiler, seeing no other VMEM in the loop, would otherwise drain the ring's prefetches before
+    // the store): they are older than every ring load the round's last step waits for.
+    constexpr bool MAT = FAMILY == FAM_MAT;
+    const MemOperand &gmo = GX ? p.xm : p.ym;
+    typedef T q4_t __attribute__((ext_vector_type(4)));
+    typedef T h16_t __attribute__((ext_vector_type(16 / sizeof(T))));
+    q4_t gmv[MAT ? WCALLS : 1];
+    auto mat_load = [&](int u, int64_t kr0, int64_t kend) __attribute__((always_inline)) {
+        const int ts = ts0 + u * SPU;
+        const int64_t kt = kr0 + ts;
+        if (kt >= kend) return;
+        const T *gp = (const T *)gmo.ptr;
+        const T *src;
+        bool full;
+        if (GK == GEN_OK) {
+            const int o = cc / (KS / 4), qd = cc % (KS / 4);
+            const int64_t row = go0 + o < gnO ? go0 + o : gnO - 1;
+            src = gp + row * gmo.so + kt * KS + 4 * qd;
+            full = gtile_full || go0 + o < gnO;
+        } else {
+            const int k = cc / (BG / 4), qo = cc % (BG / 4);
+            src = gp + (kt * KS + k) * gmo.sk + go0 + 4 * qo;
+            full = gtile_full || go0 + 4 * qo + 3 < gnO;
+        }
+        q4_t v;
+        if (full || GK == GEN_OK) {   // (GEN_OK: a row past the operand reads its last row, zeroed below)
+            if constexpr (TRI == 5) {
+                h16_t h[4 / (16 / sizeof(T))];
+#pragma unroll
+                for (int l = 0; l < 4 / (16 / (int)sizeof(T)); ++l)
+                    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(h[l]) : "v"(src + l * (16 / (int)sizeof(T))) : "memory");
+                v = __builtin_bit_cast(q4_t, h);
+            } else {
+#pragma unroll
+                for (int l = 0; l < 4 / (16 / (int)sizeof(T)); ++l) {
+                    const h16_t x = *reinterpret_cast<const h16_t *>(src + l * (16 / (int)sizeof(T)));
+#pragma unroll
+                    for (int e = 0; e < 16 / (int)sizeof(T); ++e) v[l * (16 / (int)sizeof(T)) + e] = x[e];
+                }
+            }
+        } else {   // GEN_OO quad crossing the operand's last row (TRI 5: after the ring's waits)
+            const int64_t ob = go0 + 4 * (cc % (BG / 4));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = ob + e < gnO ? src[e] : (T)0;
+        }
+        gmv[u] = v;
+    };
+    // the LDS placement of a call's 4 values (the draw's, below)
+    auto gput = [&](const T (&v)[4], int half, int ts) __attribute__((always_inline)) {
+        char *G = gslot(half, ts);
+        if (GK == GEN_OK) {
+            const int o = cc / (KS / 4), qd = cc % (KS / 4);
+#pragma unroll
+            for (int hsl = 0; hsl < 4 / EPS; ++hsl) {
+                const int q = qd * (4 / EPS) + hsl;
+                T *dst = (T *)(G + o * 128 + 16 * (q ^ sw32(o)));
+#pragma unroll
+                for (int e = 0; e < EPS; ++e) dst[e] = v[hsl * EPS + e];
+            }
+        } else {
+            const int k = cc / (BG / 4), qo = cc % (BG / 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int o = 4 * qo + e;
+                *(T *)(G + o * 128 + 16 * ((k / EPS) ^ sw32(o)) + (int)sizeof(T) * (k % EPS)) = v[e];
+            }
+        }
+    };
+    auto mat_store = [&](int u, int64_t kr0, int half, int64_t kend) __attribute__((always_inline)) {
+        const int ts = ts0 + u * SPU;
+        if (kr0 + ts >= kend) return;
+        T v[4];
+        if constexpr (TRI == 5) vm_fence4(gmv[u]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = gmv[u][e];
+        if (GK == GEN_OK) {
+            const int o = cc / (KS / 4);
+            if (!gtile_full && go0 + o >= gnO) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = (T)0;
+            }
+        }
+        gput(v, half, ts);
+    };
     // draw call u of the round starting at step kr0 into ring half `half` (steps >= kend: nothing)
     auto draw = [&](int u, int64_t kr0, int half, int64_t kend) {
+        if constexpr (MAT) {
+            mat_load(u, kr0, kend);
+            if constexpr (TRI == 5) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            mat_store(u, kr0, half, kend);
+            return;
+        }
         const int ts = ts0 + u * SPU;
         const int64_t kt = kr0 + ts;
         if (kt >= kend) return;   // (uniform per wave: ts0 is per wave for CPS >= 64)
@@ -1499,7 +1600,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
         rb::ctr_add(cbase, (uint64_t)kt * cstep, ct);
         const rb::u32x4 w = rb::philox4x32_uk<10>(ct[0], ct[1], ct[2], ct[3], gop.key[0], gop.key[1]);
         float sm[4];
-        rb::sample4<FAMILY>(w, sm, tab);
+        rb::sample4<MAT ? rb::GAUSSIAN : FAMILY>(w, sm, tab);
         T v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = FAMILY == rb::UNIFORM ? (T)sm[e] * (T)gop.scale : (T)sm[e];
@@ -1573,6 +1674,12 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
         for (int ts = 0; ts < R; ++ts) {
             const int64_t kt = kr0 + ts;
             if (kt >= kt1) break;
+            if constexpr (MAT) {   // the next round's loaded tiles: issued now, stored after the last step
+                if (ts == 0 && rd + 1 < nrounds) {
+#pragma unroll
+                    for (int u = 0; u < WCALLS; ++u) mat_load(u, kr0 + R, kt1);
+                }
+            }
             // one-triangle operand: this step's and the next one's classes and offsets (the next
             // step's part-blocks are the ones the prefetches of this step load)
             const TriStep tsc = tri_step(kt), tsn = tri_step(kt + 1 < kt1 ? kt + 1 : kt);
@@ -1646,9 +1753,16 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
             // the next round's generated tiles: every wave's share, spread over the round (f64: its
             // one call after step 1; f32: one call after every step)
             if (rd + 1 < nrounds) {
+                if constexpr (MAT) {
+                    if (ts == R - 1) {
+#pragma unroll
+                        for (int u = 0; u < WCALLS; ++u) mat_store(u, kr0 + R, half ^ 1, kt1);
+                    }
+                } else {
 #pragma unroll
                 for (int u = 0; u < WCALLS; ++u)
                     if (ts == (u * R) / WCALLS + (WCALLS == 1 ? 1 : 0)) draw(u, kr0 + R, half ^ 1, kt1);
+                }
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -2269,6 +2383,31 @@ static bool stream_t_ok(const GemmProblem &p) {
     return (5 * KS * m.sk + mnO + 256) * (int64_t)sizeof(T) < ((int64_t)1 << 32);
 }
 
+// Both operands in memory (an operator with a buffer, S.buff; a Threefry window drawn into a
+// workspace): the operand with fewer outer indices (the operator, for a sketch) takes the generated
+// operand's place in the streamed kernel, read from memory (FAM_MAT) into the LDS slots the draw
+// fills, so the explicit operator gives the drawn one's bits on the same geometry. It needs rows
+// contiguous along k (GEN_OK form) or along o (GEN_OO form) at 16-B alignment, and the other operand
+// streamable (stream_ok: along k; stream_t_ok: along o). Otherwise skge_gemm_kernel (PLAN_GENERIC).
+template <typename T>
+static bool mat_problem(const GemmProblem &p, GemmProblem &q, int &gk, bool &gx, int &tri) {
+    if (p.xkind != MEM || p.ykind != MEM || p.tri || p.materialise) return false;
+    gx = p.M <= p.N;
+    const MemOperand &g = gx ? p.xm : p.ym;
+    const int64_t E = 16 / (int64_t)sizeof(T);
+    if (((uintptr_t)g.ptr & 15) != 0) return false;
+    if (g.sk == 1 && g.so % E == 0) gk = GEN_OK;
+    else if (g.so == 1 && g.sk % E == 0) gk = GEN_OO;
+    else return false;
+    q = p;
+    (gx ? q.xkind : q.ykind) = gk;
+    (gx ? q.xg : q.yg) = GenOperand{};
+    if (stream_ok<T>(q)) tri = 0;
+    else if (stream_t_ok<T>(q)) tri = 5;
+    else return false;
+    return true;
+}
+
 // Which kernel launch_gemm runs for p, with its tiles and split (the same tests, in the same order).
 template <typename T>
 static GemmPlan plan_gemm(const GemmProblem &p) {
@@ -2280,6 +2419,12 @@ static GemmPlan plan_gemm(const GemmProblem &p) {
         if (q.xkind != MEM && q.xg.rng == rb::RNG_THREEFRY) threefry_as_mem<T>(q, true, nullptr);
         if (q.ykind != MEM && q.yg.rng == rb::RNG_THREEFRY) threefry_as_mem<T>(q, false, nullptr);
         return plan_gemm<T>(q);
+    }
+    {
+        GemmProblem q;
+        int gk, tri;
+        bool gx;
+        if (mat_problem<T>(p, q, gk, gx, tri)) return plan_gemm<T>(q);   // as launch_gemm_mat
     }
     if (!p.tri && gemv_ok(p)) {   // one vector operand: sketch_vector (skve.hip)
         pl.kernel = PLAN_GEMV;
@@ -2380,7 +2525,29 @@ static hipError_t launch_gemm_threefry(const GemmProblem &p, hipStream_t s) {
 }
 
 template <typename T>
+static hipError_t launch_gemm_mat(const GemmProblem &q, int gk, bool gx, int tri, hipStream_t s) {
+#define RBH_MAT_L(GK, GX, TRI)                                                                  \
+    if (gk == GK && gx == GX && tri == TRI) return launch_stream<T, GK, FAM_MAT, GX, TRI>(q, s)
+    RBH_MAT_L(GEN_OK, true, 0);
+    RBH_MAT_L(GEN_OK, false, 0);
+    RBH_MAT_L(GEN_OO, true, 0);
+    RBH_MAT_L(GEN_OO, false, 0);
+    RBH_MAT_L(GEN_OK, true, 5);
+    RBH_MAT_L(GEN_OK, false, 5);
+    RBH_MAT_L(GEN_OO, true, 5);
+    RBH_MAT_L(GEN_OO, false, 5);
+#undef RBH_MAT_L
+    return hipErrorInvalidValue;
+}
+
+template <typename T>
 static hipError_t launch_gemm(const GemmProblem &p, hipStream_t s) {
+    {   // both operands in memory: the streamed kernel with the operator read from memory
+        GemmProblem q;
+        int gk, tri;
+        bool gx;
+        if (mat_problem<T>(p, q, gk, gx, tri)) return launch_gemm_mat<T>(q, gk, gx, tri, s);
+    }
     // (a one-triangle read needs a generated operand: the caller symmetrizes and calls again)
     if (p.tri && threefry_gen(p)) return hipErrorNotSupported;
     if (threefry_gen(p) && !gemv_ok(p)) return launch_gemm_threefry<T>(p, s);
@@ -2533,6 +2700,22 @@ RBH_STREAM_INST(double, GEN_OK, 1)
 RBH_STREAM_INST(double, GEN_OK, 2)
 RBH_STREAM_INST(double, GEN_OK, 3)
 RBH_STREAM_INST(double, GEN_OK, 4)
+#elif defined(RBH_STREAM_PART) && (RBH_STREAM_PART == 5 || RBH_STREAM_PART == 6)
+// parts 5 (f64) and 6 (f32): operators read from memory (FAM_MAT), both memory-operand forms
+#define RBH_STREAM_INST_MAT(T, GK, TRI)                                                                  \
+    template hipError_t launch_stream<T, GK, FAM_MAT, true, TRI>(const GemmProblem &, hipStream_t);      \
+    template hipError_t launch_stream<T, GK, FAM_MAT, false, TRI>(const GemmProblem &, hipStream_t);
+#if RBH_STREAM_PART == 5
+#define RBH_MAT_T double
+#else
+#define RBH_MAT_T float
+#endif
+RBH_STREAM_INST_MAT(RBH_MAT_T, GEN_OK, 0)
+RBH_STREAM_INST_MAT(RBH_MAT_T, GEN_OO, 0)
+RBH_STREAM_INST_MAT(RBH_MAT_T, GEN_OK, 5)
+RBH_STREAM_INST_MAT(RBH_MAT_T, GEN_OO, 5)
+#undef RBH_MAT_T
+#undef RBH_STREAM_INST_MAT
 #endif
 #undef RBH_STREAM_INST
 

@@ -311,6 +311,63 @@ def test_materialised_equals_drawn_bitwise(cuda, dtype):
     assert np.array_equal(out[0].view(ut), out[1].view(ut))
 
 
+# An operator with a buffer (S.buff: fill_dense(S), a Threefry window, BlackBox data) in the
+# streamed kernel (FAM_MAT): read from memory into the LDS slots the in-kernel draw fills, so on the
+# same geometry (tile shape and split: functions of the shape only) the explicit operator gives the
+# drawn operator's bits. Buffer rows along k (GEN_OK form) or along o (GEN_OO form), memory operand
+# along k (stream) or along o (stream_t), unsplit 32 x 1024 grids, split small grids, ragged d.
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("layout", ["C", "R"])
+@pytest.mark.parametrize("buf_layout", ["C", "R"])
+@pytest.mark.parametrize("opS", ["N", "T"])
+@pytest.mark.parametrize("shape", [(132, 2600, 512), (512, 16384, 256), (96, 1100, 1024)])
+def test_explicit_operator_streams_bitwise(cuda, dtype, layout, buf_layout, opS, shape):
+    d, n, m = shape
+    SR, SC = (d, m) if opS == "N" else (m, d)
+    D = rb.DenseDist(SR, SC)
+    A = dev(O.random_matrix(m, n, 99, dtype), cuda)
+    lda, ldb = (m, d) if layout == "C" else (n, n)
+    buf = torch.empty(SR * SC, dtype=A.dtype, device=cuda)
+    rb.fill_dense(buf_layout, D, SR, SC, 0, 0, buf, rb.RNGState(5))
+    out = []
+    for explicit in (False, True):
+        S = rb.DenseSkOp(D, rb.RNGState(5))
+        if explicit:
+            S.buff, S.buff_layout = buf, buf_layout
+        plan = rb.plan_left(layout, opS, "N", d, n, m, S, A, lda, ldb, dtype="f64" if dtype == np.float64 else "f32")
+        assert plan.kernel in ("stream", "stream_t"), plan
+        B = torch.full((d * n,), float("nan"), dtype=A.dtype, device=cuda)
+        rb.sketch_general_left(layout, opS, "N", d, n, m, dtype(1.0), S, A, lda, dtype(0.0), B, ldb)
+        out.append(host(B))
+    ut = np.uint64 if dtype == np.float64 else np.uint32
+    assert not np.isnan(out[1]).any()
+    assert np.array_equal(out[0].view(ut), out[1].view(ut)), f"{np.sum(out[0] != out[1])} of {out[0].size} differ"
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("layout", ["C", "R"])
+@pytest.mark.parametrize("buf_layout", ["C", "R"])
+def test_explicit_operator_right_sketch_bitwise(cuda, dtype, layout, buf_layout):
+    """B = A S with S.buff (the operator the Y / transposed side): the drawn operator's bits."""
+    m, d, n = 1100, 96, 1024
+    D = rb.DenseDist(n, d)
+    A = dev(O.random_matrix(m, n, 57, dtype), cuda)
+    lda, ldb = (m, m) if layout == "C" else (n, d)
+    buf = torch.empty(n * d, dtype=A.dtype, device=cuda)
+    rb.fill_dense(buf_layout, D, n, d, 0, 0, buf, rb.RNGState(8))
+    out = []
+    for explicit in (False, True):
+        S = rb.DenseSkOp(D, rb.RNGState(8))
+        if explicit:
+            S.buff, S.buff_layout = buf, buf_layout
+        B = torch.full((m * d,), float("nan"), dtype=A.dtype, device=cuda)
+        rb.sketch_general_right(layout, "N", "N", m, d, n, dtype(1.0), A, lda, S, dtype(0.0), B, ldb)
+        out.append(host(B))
+    ut = np.uint64 if dtype == np.float64 else np.uint32
+    assert not np.isnan(out[1]).any()
+    assert np.array_equal(out[0].view(ut), out[1].view(ut)), f"{np.sum(out[0] != out[1])} of {out[0].size} differ"
+
+
 # Split-K on the wide kernels (What the multi-GPU dense runs execute: a rank's column chunk of
 # BASELINE configs[3] has 64 wide tiles and runs the f32 32-deep kernel split 4). d = 128, m = n =
 # 4096: automatic split 16 (f32) / 8 (f64, 32 x 512 tiles); forced 1 (unsplit) and 3 (uneven
