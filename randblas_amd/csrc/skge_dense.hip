@@ -1220,7 +1220,7 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     constexpr int EPS = 16 / (int)sizeof(T);              // elements per 16-B slot
     constexpr int BMW = MW;                               // memory rows per wave (128; f64 64)
     constexpr int FA = BG / 16, FB = BMW / 16;            // FA x FB MFMA tiles per wave
-    constexpr int R = 4;                                  // steps per round
+    constexpr int R = sizeof(T) == 8 ? RBH_STREAM_R : 4;  // steps per round
     constexpr int SLOT_B = BG * 128;                      // bytes per generated tile (BG rows x 128 B)
     constexpr int CPS = BG * KS / 4;                      // Philox calls per step (f64 128, f32 512)
     constexpr int SPU = 512 / CPS;                        // steps between a lane's calls of a round
@@ -2405,6 +2405,11 @@ static bool mat_problem(const GemmProblem &p, GemmProblem &q, int &gk, bool &gx,
     if (stream_ok<T>(q)) tri = 0;
     else if (stream_t_ok<T>(q)) tri = 5;
     else return false;
+    // f64 rows along o with a memory operand along k: 64 x 512 tiles (its 32 x 1024 kernels spill 6-16
+    // registers a lane): NS ColMajor with a ColMajor buffer 15.19-15.25 ms against 15.83; with the
+    // transposed memory operand the 32 x 1024 tiles stay (15.11 against 15.54-15.56; same box, two
+    // alternations, profiles/r06/ab_mat_oo64.txt)
+    if (gk == GEN_OO && tri == 0 && sizeof(T) == 8) q.beside = 1;
     return true;
 }
 

@@ -35,6 +35,12 @@
 #define RBH_TRI_STREAMED 1
 #endif
 
+// steps per round of the streamed f64 kernel (one barrier per round; the next round's generated tiles
+// are drawn during the round)
+#ifndef RBH_STREAM_R
+#define RBH_STREAM_R 4
+#endif
+
 // ---- saso.hip: the LDS-DMA SASO apply (saso_dma_kernel) --------------------------------------
 // log2 of the chunk depth (contracted indices per panel): 7 (64-deep chunks: 0.70-0.84 ms on C3)
 #ifndef SD_KCS_DEF
