@@ -1220,7 +1220,11 @@ __global__ __launch_bounds__(512) void skge_stream_kernel(const GemmProblem p) {
     constexpr int EPS = 16 / (int)sizeof(T);              // elements per 16-B slot
     constexpr int BMW = MW;                               // memory rows per wave (128; f64 64)
     constexpr int FA = BG / 16, FB = BMW / 16;            // FA x FB MFMA tiles per wave
-    constexpr int R = sizeof(T) == 8 ? RBH_STREAM_R : 4;  // steps per round
+    // steps per round (variants.hpp): f64 32-row tiles and one-triangle operands 8, else 4 (an operator
+    // read from memory, FAM_MAT, holds its loaded values across the round: 4, its 32 x 1024 kernels
+    // spill 10-51 registers a lane with 8)
+    constexpr int R = sizeof(T) != 8 || FAMILY == FAM_MAT ? 4
+                    : BG == 32 ? RBH_STREAM_R32 : (TRI >= 1 && TRI <= 4) ? RBH_STREAM_RTRI : 4;
     constexpr int SLOT_B = BG * 128;                      // bytes per generated tile (BG rows x 128 B)
     constexpr int CPS = BG * KS / 4;                      // Philox calls per step (f64 128, f32 512)
     constexpr int SPU = 512 / CPS;                        // steps between a lane's calls of a round

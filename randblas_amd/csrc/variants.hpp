@@ -36,9 +36,17 @@
 #endif
 
 // steps per round of the streamed f64 kernel (one barrier per round; the next round's generated tiles
-// are drawn during the round)
-#ifndef RBH_STREAM_R
-#define RBH_STREAM_R 4
+// are drawn during it; the LDS ring holds two rounds). 32-row tiles 8 (NS 15.32-15.34 ms against
+// 15.36-15.41, NS RowMajor 15.36-15.38 against 15.47-15.51, C2 7.672-7.677 against 7.690-7.702; 16:
+// a kilobyte a lane of spills), one-triangle operands 8 (C5p 4.161-4.164 ms against 4.223-4.227);
+// the 64 x 512 tiles of a full-storage operand keep 4: beside sketch_symmetric's check a 128-KiB
+// ring leaves it no LDS (C5 step 4.56-4.78 ms against 4.17-4.20). Same box, alternating
+// (profiles/r06/ab_stream_r8.jsonl, ab_stream_r8_bench.jsonl).
+#ifndef RBH_STREAM_R32
+#define RBH_STREAM_R32 8
+#endif
+#ifndef RBH_STREAM_RTRI
+#define RBH_STREAM_RTRI 8
 #endif
 
 // ---- saso.hip: the LDS-DMA SASO apply (saso_dma_kernel) --------------------------------------
