@@ -2333,20 +2333,18 @@ static bool tri_ok(const GemmProblem &p) {
     return last * (int64_t)sizeof(double) < ((int64_t)1 << 32);
 }
 
-// One-triangle symmetric memory operand: the wide f64 kernel when the generated operand runs its
-// counter along k from a Philox quad (GEN_OK, every MajorAxis::Long operator) and K % 16 == 0; full
-// storage also needs 16-B aligned rows. Otherwise hipErrorNotSupported, and the caller expands
-// the triangle (launch_symmetrize) and runs the plain kernels.
-// A Threefry operator (RNGState<r123::Threefry4x32>, base.hh:153-161) in a GEMM problem: the GEMM
-// kernels draw Philox4x32 only (the generator sits on their critical issue path), so such a window
-// is drawn by fill_dense into a workspace first, element (o, k) at buf[o K + k], and the problem
-// runs with it as a memory operand -- the reference's fill_dense + gemm shape (skge.hh:173-215). The
-// gemv kernel (sketch_vector) draws either generator itself.
+// Generated windows drawn into a workspace first (launch_gemm_drawn_first): a Threefry operator
+// (RNGState<r123::Threefry4x32>, base.hh:153-161) -- the GEMM kernels draw Philox4x32 only (the
+// generator sits on their critical issue path) -- and, with rbh_options.materialise, a Philox one.
+// fill_dense writes element (o, k) at buf[o K + k] and the problem runs with it as an operator in
+// memory (FAM_MAT, launch_gemm_mat): the reference's fill_dense + gemm shape (skge.hh:173-215), with
+// the drawn kernel's bits. The gemv kernel (sketch_vector) draws either generator itself; a
+// materialised one-triangle problem keeps the wide kernel's GMAT form (launch_wide_tri).
 static bool threefry_gen(const GemmProblem &p) {
     return (p.xkind != MEM && p.xg.rng == rb::RNG_THREEFRY) || (p.ykind != MEM && p.yg.rng == rb::RNG_THREEFRY);
 }
 template <typename T>
-static void threefry_as_mem(GemmProblem &q, bool gx, const void *buf) {
+static void window_as_mem(GemmProblem &q, bool gx, const void *buf) {
     int &kind = gx ? q.xkind : q.ykind;
     int &mode = gx ? q.xmode : q.ymode;
     MemOperand &m = gx ? q.xm : q.ym;
@@ -2356,7 +2354,53 @@ static void threefry_as_mem(GemmProblem &q, bool gx, const void *buf) {
     m.sk = 1;
     mode = (q.K % (16 / (int64_t)sizeof(T))) == 0 ? 2 : 1;   // (workspaces are 256-B aligned)
 }
+template <typename T>
+static bool mat_problem(const GemmProblem &p, GemmProblem &q, int &gk, bool &gx, int &tri);
+// the problem with its drawn-first windows as memory operands (buffers at a 256-B aligned stand-in
+// address: the plan looks at alignment only); whether it takes that route
+// A Philox window the drawing kernels cannot take (a window that does not start on a Philox quad
+// along the counter, K off the step depth with f64, ...: the generic kernel, 4-66 % of the f64 peak)
+// is drawn first as well when the call is large enough (GEN_FIRST_FLOPS) and the window then streams:
+// the reference's own fill_dense + gemm, with the streamed kernel.
+constexpr double GEN_FIRST_FLOPS = 1e9;
+template <typename T> static bool stream_t_ok(const GemmProblem &p);
+template <typename T> static bool wide32_ok(const GemmProblem &p);
+static bool fused_ok(const GemmProblem &p);
+template <typename T>
+static bool drawn_first(const GemmProblem &p, GemmProblem &q) {
+    if (gemv_ok(p) || p.tri || (p.xkind == MEM) == (p.ykind == MEM)) return false;
+    GemmProblem d = p;   // the call as drawn (materialise does not change which calls take this route)
+    d.materialise = 0;
+    const bool generic = !threefry_gen(p) && !stream_ok<T>(d) && !stream_t_ok<T>(d) && !wide_ok<T>(d) &&
+                         !wide32_ok<T>(d) && !fused_ok(d) &&
+                         2.0 * (double)p.M * (double)p.N * (double)p.K >= GEN_FIRST_FLOPS;
+    if (!(threefry_gen(p) || p.materialise || generic)) return false;
+    q = p;
+    for (int side = 0; side < 2; ++side)
+        if ((side == 0 ? p.xkind : p.ykind) != MEM) window_as_mem<T>(q, side == 0, (const void *)(uintptr_t)256);
+    q.materialise = 0;
+    if (threefry_gen(p)) return true;   // (on the generic kernel if it does not stream)
+    if (generic) {
+        GemmProblem r;
+        int gk, tri;
+        bool gx;
+        return mat_problem<T>(q, r, gk, gx, tri);
+    }
+    // materialise: only where the drawn problem streams too, on the geometry the window then takes,
+    // so the option keeps the drawn operator's bits (elsewhere the older route, wide GMAT / in place)
+    GemmProblem r;
+    if (!stream_ok<T>(d) && !stream_t_ok<T>(d)) return false;
+    int gk, tri;
+    bool gx;
+    if (!mat_problem<T>(q, r, gk, gx, tri)) return false;
+    const StreamGeom a = stream_geom<T>(d), b = stream_geom<T>(r);
+    return a.bg == b.bg && a.mw == b.mw && a.split == b.split && (gx == (p.xkind != MEM));
+}
 
+// One-triangle symmetric memory operand: the wide f64 kernel when the generated operand runs its
+// counter along k from a Philox quad (GEN_OK, every MajorAxis::Long operator) and K % 16 == 0; full
+// storage also needs 16-B aligned rows. Otherwise hipErrorNotSupported, and the caller expands
+// the triangle (launch_symmetrize) and runs the plain kernels.
 template <typename T>
 static hipError_t launch_gemm_tri(const GemmProblem &p, hipStream_t s) {
     if (!tri_ok<T>(p)) return hipErrorNotSupported;
@@ -2423,11 +2467,9 @@ static GemmPlan plan_gemm(const GemmProblem &p) {
     GemmPlan pl{PLAN_NONE, 1, 0, 0};
     if (p.M <= 0 || p.N <= 0) return pl;
     if (p.K <= 0 || p.alpha == 0.0) { pl.kernel = PLAN_SCALE; return pl; }
-    if (threefry_gen(p) && !gemv_ok(p)) {   // as launch_gemm_threefry: the window drawn first
-        GemmProblem q = p;
-        if (q.xkind != MEM && q.xg.rng == rb::RNG_THREEFRY) threefry_as_mem<T>(q, true, nullptr);
-        if (q.ykind != MEM && q.yg.rng == rb::RNG_THREEFRY) threefry_as_mem<T>(q, false, nullptr);
-        return plan_gemm<T>(q);
+    {   // as launch_gemm_drawn_first: the window drawn into a workspace first
+        GemmProblem q;
+        if (drawn_first<T>(p, q)) return plan_gemm<T>(q);
     }
     {
         GemmProblem q;
@@ -2503,15 +2545,16 @@ template <typename T>
 static hipError_t launch_gemm(const GemmProblem &p, hipStream_t s);
 
 template <typename T>
-static hipError_t launch_gemm_threefry(const GemmProblem &p, hipStream_t s) {
+static hipError_t launch_gemm_drawn_first(const GemmProblem &p, hipStream_t s) {
     GemmProblem q = p;
+    q.materialise = 0;
     void *bufs[2] = {nullptr, nullptr};
     hipError_t e = hipSuccess;
     for (int side = 0; side < 2 && e == hipSuccess; ++side) {
         const bool gx = side == 0;
+        if ((gx ? p.xkind : p.ykind) == MEM) continue;   // (drawn_first: every generated side)
         const int kind = gx ? p.xkind : p.ykind;
         const GenOperand &g = gx ? p.xg : p.yg;
-        if (kind == MEM || g.rng != rb::RNG_THREEFRY) continue;
         const int64_t nO = gx ? p.M : p.N;
         e = ws_alloc(&bufs[side], sizeof(T) * (size_t)nO * (size_t)p.K, s);
         if (e != hipSuccess) break;
@@ -2522,7 +2565,7 @@ static hipError_t launch_gemm_threefry(const GemmProblem &p, hipStream_t s) {
         else
             e = kind == GEN_OK ? launch_fill_dense_f32(g, nO, p.K, 0, (float *)bufs[side], s)
                                : launch_fill_dense_f32(g, p.K, nO, 1, (float *)bufs[side], s);
-        threefry_as_mem<T>(q, gx, bufs[side]);
+        window_as_mem<T>(q, gx, bufs[side]);
     }
     if (e == hipSuccess) e = launch_gemm<T>(q, s);
     for (void *b : bufs)
@@ -2559,7 +2602,10 @@ static hipError_t launch_gemm(const GemmProblem &p, hipStream_t s) {
     }
     // (a one-triangle read needs a generated operand: the caller symmetrizes and calls again)
     if (p.tri && threefry_gen(p)) return hipErrorNotSupported;
-    if (threefry_gen(p) && !gemv_ok(p)) return launch_gemm_threefry<T>(p, s);
+    {
+        GemmProblem q;
+        if (drawn_first<T>(p, q)) return launch_gemm_drawn_first<T>(p, s);
+    }
     if (p.tri) return launch_gemm_tri<T>(p, s);
     const bool unif = (p.xkind != MEM ? p.xg.family : p.yg.family) == rb::UNIFORM;
     const int kernel = plan_gemm<T>(p).kernel;

@@ -214,10 +214,11 @@ def test_plan_options_fix_the_split():
     assert _plan(1024, 16384, 16384, layout="R", dtype="f32") == rb.Plan("stream_t", p32.splitk, p32.tiles, p32.workgroups)
     assert _plan(256, 4096, 4004, layout="R", dtype="f32").kernel == "generic"
     assert _plan(1024, 32768, 32768, layout="R").kernel == "stream_t"
-    # the materialised window: the 64 x 512 kernels that load it (the same sums)
-    assert _plan(1024, 16384, 16384, opts=rb.Options(materialise=True)).kernel == "wide"
-    # (the f32 materialised kernel takes the streamed kernel's split: the same bits)
-    assert _plan(256, 32768, 32768, dtype="f32", opts=rb.Options(materialise=True)) == rb.Plan("wide32", 2, 256, 512)
+    # the materialised window: drawn into a workspace, then read by the streamed kernel (FAM_MAT) on
+    # the drawn call's geometry (the same sums)
+    assert _plan(1024, 16384, 16384, opts=rb.Options(materialise=True)) == _plan(1024, 16384, 16384)
+    assert _plan(256, 32768, 32768, dtype="f32", opts=rb.Options(materialise=True)) == _plan(256, 32768, 32768, dtype="f32")
+    assert _plan(1024, 16384, 16384, layout="R", opts=rb.Options(materialise=True)) == rb.Plan("stream_t", 1, 512, 512)
     # f32 with K not a multiple of 32: the fused kernel
     assert _plan(256, 4096, 4004, dtype="f32").kernel == "fused"
     with pytest.raises(rb.RandBLASError) as ei:

@@ -270,7 +270,8 @@ def test_row_shards_reassemble(cuda):
 
 # Memory operands spanning >= 4 wide tiles (here 2100 outer indices): the drawing wide kernels (the
 # default: the operator tile is regenerated in LDS and never stored) and, with Options(materialise),
-# the opt-in materialised-operator kernels (gen_fill_kernel + the GMAT wide kernels). Generated rows not
+# the opt-in materialised operator (fill_dense into a workspace, then the streamed kernel reading it:
+# FAM_MAT). Generated rows not
 # a multiple of 64, a ragged last tile, a submatrix window, both families and major axes, f64 and
 # f32 (K = 256 is a multiple of both step depths), left and right sketches.
 @pytest.fixture(params=["draw", "materialise"])
@@ -296,7 +297,7 @@ def test_rskge3_wide_tiles(cuda, operator_mode, dtype, layout, fam, maj):
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_materialised_equals_drawn_bitwise(cuda, dtype):
-    """The opt-in materialised window feeds the wide kernel the same LDS image in the same MFMA
+    """The opt-in materialised window feeds the streamed kernel the same LDS image in the same MFMA
     order as the in-kernel draw: bitwise the same sketch."""
     d, n, m = 130, 2600, 512
     A = dev(O.random_matrix(m, n, 99, dtype), cuda)
@@ -342,6 +343,41 @@ def test_explicit_operator_streams_bitwise(cuda, dtype, layout, buf_layout, opS,
     ut = np.uint64 if dtype == np.float64 else np.uint32
     assert not np.isnan(out[1]).any()
     assert np.array_equal(out[0].view(ut), out[1].view(ut)), f"{np.sum(out[0] != out[1])} of {out[0].size} differ"
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("layout", ["C", "R"])
+@pytest.mark.parametrize("ro,co", [(1, 3), (0, 2), (5, 1)])
+def test_unaligned_window_drawn_first(cuda, dtype, layout, ro, co):
+    """A window that does not start on a Philox quad along the counter cannot be drawn by the
+    streamed kernels; a large call draws it into a workspace first and streams it (FAM_MAT): the
+    same bits as an explicit operator holding exactly that window, and within E of the oracle."""
+    d, n, m = 256, 2048, 4096
+    D = rb.DenseDist(d + 7, m + 9)
+    A = dev(O.random_matrix(m, n, 99, dtype), cuda)
+    lda, ldb = (m, d) if layout == "C" else (n, n)
+    tag = "f64" if dtype == np.float64 else "f32"
+    S = rb.DenseSkOp(D, rb.RNGState(4))
+    assert rb.plan_left(layout, "N", "N", d, n, m, S, A, lda, ldb, ro_s=ro, co_s=co, dtype=tag).kernel in ("stream", "stream_t")
+    win = torch.empty(d * m, dtype=A.dtype, device=cuda)
+    rb.fill_dense("R", D, d, m, ro, co, win, rb.RNGState(4))
+    W = rb.DenseSkOp(rb.DenseDist(d, m), rb.RNGState(4))
+    W.buff, W.buff_layout = win, "R"
+    out = []
+    for op, kw in ((S, dict(ro_s=ro, co_s=co)), (W, {})):
+        B = torch.full((d * n,), float("nan"), dtype=A.dtype, device=cuda)
+        rb.sketch_general_left(layout, "N", "N", d, n, m, dtype(1.0), op, A, lda, dtype(0.0), B, ldb, **kw)
+        out.append(host(B))
+    ut = np.uint64 if dtype == np.float64 else np.uint32
+    assert np.array_equal(out[0].view(ut), out[1].view(ut)), f"{np.sum(out[0] != out[1])} differ"
+    # within E of the oracle on a column slice
+    js = slice(0, 64)
+    Am = host(A).reshape(n, m).T if layout == "C" else host(A).reshape(m, n)
+    Wm = host(win).reshape(d, m).astype(np.float64)
+    exp = Wm @ Am[:, js].astype(np.float64)
+    Bm = out[0].reshape(n, d).T if layout == "C" else out[0].reshape(d, n)
+    E = m * 2 * np.finfo(dtype).eps * (np.abs(Wm) @ np.abs(Am[:, js].astype(np.float64)))
+    assert np.all(np.abs(Bm[:, js] - exp) <= E)
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
@@ -412,13 +448,14 @@ def test_f32_split_chunks_bitwise_with_whole_split(cuda):
     assert np.array_equal(got.view(np.uint32), exp.view(np.uint32))
 
 
-# The streamed wide kernel (32 or 64 x 1024 tiles, memory operand straight to registers) adds every
-# output element's terms in the same MFMA order as the 64 x 512 wide kernels, which the
-# materialised-window option still runs: bitwise equal across operand orientations (left/right x
-# layouts: the generated operand as X or Y), counter directions (major axis), families, ragged tiles,
-# split-K, and both streamed tile heights (f32 "bg64": 64 x 1024 tiles unsplit, "bg64split": split 16;
-# f64 "f64bg32split": a small grid on 32 x 512 tiles, 24 tiles split 10 against the 64 x 512 wide
-# kernel's 12 tiles run with that split).
+# The streamed kernel drawing the operator (the default) against the materialised-window option
+# (fill_dense into a workspace, then the streamed kernel reading it: FAM_MAT, the rows of the window
+# along k): the same geometry, the same LDS tiles, the same MFMA order, so bitwise equal across
+# operand orientations (left/right x layouts: the generated operand as X or Y), counter directions
+# (major axis), families, ragged tiles, split-K, and the tile heights (f32 "bg64": 64 x 1024 tiles
+# unsplit, "bg64split": split 16; f64 "f64bg32split": a small grid on 32 x 512 tiles, split 10).
+# (Until round 6 the option ran the 64 x 512 wide kernels, which this test held to the same bits;
+# they remain for one-triangle operands, tests/test_gpu_sksy.py.)
 STREAM_SHAPES = {"ragged": (100, 2100, 256), "split": (64, 1100, 4096), "bg64": (1000, 9000, 256),
                  "bg64split": (250, 4000, 4096), "f64bg32split": (122, 3000, 4096)}
 
@@ -427,7 +464,7 @@ STREAM_SHAPES = {"ragged": (100, 2100, 256), "split": (64, 1100, 4096), "bg64": 
 @pytest.mark.parametrize("side,layout", [("L", "C"), ("L", "R"), ("R", "C"), ("R", "R")])
 @pytest.mark.parametrize("fam,maj", [("G", "L"), ("G", "S"), ("U", "L")])
 @pytest.mark.parametrize("shape", sorted(STREAM_SHAPES))
-def test_stream_kernel_equals_wide_bitwise(cuda, dtype, side, layout, fam, maj, shape):
+def test_stream_kernel_equals_materialised_bitwise(cuda, dtype, side, layout, fam, maj, shape):
     d, n, m = STREAM_SHAPES[shape]
     if shape.startswith("f64") and dtype != np.float64:
         pytest.skip("an f64 tile-geometry case")
@@ -456,10 +493,8 @@ def test_stream_kernel_equals_wide_bitwise(cuda, dtype, side, layout, fam, maj, 
             rb.sketch_general_right(layout, opA, "N", n, d, m, dtype(1.5), A, m, S, dtype(-0.5), B, ldb, ro_s=8,
                                     co_s=4, options=opts)
         out.append(host(B))
-    if dtype == np.float64 and plans[0].kernel == "wide":
-        pytest.skip("f64 runs the 64 x 512 wide kernel (this build does not stream f64)")
-    assert plans[0].kernel == "stream" and plans[1].kernel in ("wide", "wide32"), plans
-    assert plans[0].splitk == plans[1].splitk and (plans[0].splitk > 1) == shape.endswith("split"), plans
+    assert plans[0].kernel == "stream" and plans[1] == plans[0], plans
+    assert (plans[0].splitk > 1) == shape.endswith("split"), plans
     if dtype == np.float32:
         bg = 64 if shape.startswith("bg64") else 32
         assert plans[0].tiles == -(-(d) // bg) * -(-n // 1024), plans

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--side", default="left", choices=["left", "right"], help="right: B (m x d) = A (m x n) S (n x d)")
     ap.add_argument("--opS", default="N", choices=["N", "T"])
     ap.add_argument("--tag", default=None, help="copied into the output line (A/B runs)")
+    ap.add_argument("--materialise", action="store_true", help="rbh_options.materialise = 1")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     tdt = torch.float64 if a.dtype == "f64" else torch.float32
@@ -40,7 +41,7 @@ def main():
         S = rb.DenseSkOp(rb.DenseDist(a.n, a.d) if a.opS == "N" else rb.DenseDist(a.d, a.n), rb.RNGState(0))
         lda, ldb = (a.m, a.m) if col else (a.n, a.d)
         B = torch.empty(a.m * a.d, dtype=tdt, device=dev)
-    opts = rb.Options(splitk=a.splitk)
+    opts = rb.Options(splitk=a.splitk, materialise=a.materialise)
 
     def call():
         if a.side == "left":
@@ -61,7 +62,7 @@ def main():
     plan = rb.plan_left(a.layout, a.opS, "N", a.d, a.n, a.m, S, A, lda, ldb, dtype=a.dtype, options=opts) if a.side == "left" else None
     flops = 2.0 * a.d * a.m * a.n
     peak = 78.6e12 if a.dtype == "f64" else 157.3e12
-    print(json.dumps({"tag": a.tag, "dtype": a.dtype, "d": a.d, "m": a.m, "n": a.n, "layout": a.layout, "side": a.side, "opS": a.opS,
+    print(json.dumps({"tag": a.tag, "materialise": a.materialise, "dtype": a.dtype, "d": a.d, "m": a.m, "n": a.n, "layout": a.layout, "side": a.side, "opS": a.opS,
                       "ms": ms, "tflops": flops / ms / 1e9, "frac": flops / ms / 1e-3 / peak,
                       "plan": plan.kernel if plan else None, "tiles": plan.tiles if plan else None,
                       "splitk": plan.splitk if plan else None}))
