@@ -70,13 +70,16 @@ struct GemmProblem {
     // overlapped check): the streamed f64 kernel keeps its 64 x 512 tiles (236 registers a wave)
     // instead of the 32 x 1024 ones (256)
     int beside;
+    // 1: no generated window is drawn into a workspace first (launch_gemm_drawn_first could not
+    // allocate one): the kernels draw it in place
+    int in_place;
 };
 
 // The kernel launch_gemm_* would run for a problem, and its split-K factor (rbh_plan).
 enum PlanKernel : int {
     PLAN_NONE = 0,        // empty output
     PLAN_SCALE = 1,       // K == 0 or alpha == 0: C = beta C only
-    PLAN_GENERIC = 2,     // skge_gemm_kernel (any operand modes, explicit S buffers)
+    PLAN_GENERIC = 2,     // skge_gemm_kernel (any operand modes; S buffers the streamed kernel cannot read)
     PLAN_FUSED = 3,       // skge_fused_kernel
     PLAN_WIDE = 4,        // skge_wide_kernel (f64)
     PLAN_WIDE32 = 5,      // skge_wide32_kernel (f32)

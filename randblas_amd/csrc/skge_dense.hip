@@ -2369,6 +2369,10 @@ static bool fused_ok(const GemmProblem &p);
 template <typename T>
 static bool drawn_first(const GemmProblem &p, GemmProblem &q) {
     if (gemv_ok(p) || p.tri || (p.xkind == MEM) == (p.ykind == MEM)) return false;
+    const double wbytes = (double)(p.xkind != MEM ? p.M : p.N) * (double)p.K * (double)sizeof(T);
+    // a Threefry window always (the kernels draw Philox only); the others up to MAT_MAX_BYTES and
+    // while a workspace can be had
+    if (!threefry_gen(p) && (p.in_place || wbytes > (double)MAT_MAX_BYTES)) return false;
     GemmProblem d = p;   // the call as drawn (materialise does not change which calls take this route)
     d.materialise = 0;
     const bool generic = !threefry_gen(p) && !stream_ok<T>(d) && !stream_t_ok<T>(d) && !wide_ok<T>(d) &&
@@ -2557,6 +2561,14 @@ static hipError_t launch_gemm_drawn_first(const GemmProblem &p, hipStream_t s) {
         const GenOperand &g = gx ? p.xg : p.yg;
         const int64_t nO = gx ? p.M : p.N;
         e = ws_alloc(&bufs[side], sizeof(T) * (size_t)nO * (size_t)p.K, s);
+        if (e != hipSuccess && !threefry_gen(p)) {   // no room: the kernels draw the window in place
+            (void)hipGetLastError();
+            for (void *b : bufs)
+                if (b) (void)ws_free(b, s);
+            GemmProblem r = p;
+            r.in_place = 1;
+            return launch_gemm<T>(r, s);
+        }
         if (e != hipSuccess) break;
         // GEN_OK: natural rows o, columns k (row-major window); GEN_OO: natural rows k, stored transposed
         if (sizeof(T) == 8)
