@@ -1498,12 +1498,14 @@ int rbh_is_device_pointer(const void *p) { return is_device_ptr(p) ? 1 : 0; }
 
 int rbh_dense_next_state(const rbh_dense_dist *D, const rbh_state *seed, rbh_state *next) {
     RBH_REQUIRE(D && seed && next);
+    RBH_REQUIRE(seed->rng == RBH_RNG_PHILOX4X32 || seed->rng == RBH_RNG_THREEFRY4X32);
     dense_next(D, seed, next);
     return RBH_OK;
 }
 
 int rbh_sparse_next_state(const rbh_sparse_dist *D, const rbh_state *seed, rbh_state *next) {
     RBH_REQUIRE(D && seed && next);
+    RBH_REQUIRE(seed->rng == RBH_RNG_PHILOX4X32 || seed->rng == RBH_RNG_THREEFRY4X32);
     // sparse::compute_next_state (sparse_skops.hh:115-126): advances by vec_nnz * minor_len with
     // minor_len = min(dims) for SASO, max(dims) for LASO (reference quirk kept).
     const int64_t minor_len = D->major_axis == 'S' ? std::min(D->n_rows, D->n_cols) : std::max(D->n_rows, D->n_cols);

@@ -236,3 +236,24 @@ def test_unpack_shards_rejects_host_pointers():
     import torch
     with pytest.raises(ValueError):
         rb.unpack_shards(torch.zeros(16, dtype=torch.float64), 2, 2, 4, torch.zeros(16, dtype=torch.float64), 4, 8)
+
+
+def test_rng_state_round_trips_through_next_state():
+    """DenseSkOp / SparseSkOp next_state keep the generator and all four key words."""
+    st = rb.RNGState(key=5, key_hi=6, rng="threefry", key_ext=(7, 8))
+    nd = rb.dense_next_state(rb.DenseDist(30, 200), st)
+    ns = rb.sparse_next_state(rb.SparseDist(30, 200, 3), st)
+    for n in (nd, ns):
+        assert n.rng == "threefry" and (n.key, n.key_hi, tuple(n.key_ext)) == (5, 6, (7, 8))
+        assert tuple(n.counter) != tuple(st.counter)
+    assert tuple(rb.dense_next_state(rb.DenseDist(30, 200), rb.RNGState(5)).counter) == tuple(nd.counter)
+
+
+def test_unknown_generator_tag_is_refused():
+    """rbh_state.rng other than RBH_RNG_PHILOX4X32 / RBH_RNG_THREEFRY4X32 fails the argument check."""
+    s = rb.RNGState(3).c()
+    s.rng = 7
+    out = rb.RNGStateC()
+    rc = rb.lib.rbh_dense_next_state(ctypes.byref(rb.DenseDist(30, 200).c()), ctypes.byref(s), ctypes.byref(out))
+    assert rc != 0
+    assert "seed->rng" in rb.lib.rbh_last_error().decode()

@@ -73,7 +73,8 @@ def op(M, o):
     return M if o == "N" else M.T
 
 
-def run_case(cuda, side, layout, fmt, opS, opA, dtype, alpha, beta, dims, offs, identity=False, density=0.08):
+def run_case(cuda, side, layout, fmt, opS, opA, dtype, alpha, beta, dims, offs, identity=False, density=0.08,
+             rng="philox"):
     eps = np.finfo(dtype).eps
     ro_s, co_s, ro_a, co_a = offs
     if side == "left":   # B (d x n) = op(Ssub) (d x m) op(Asub) (m x n)
@@ -97,7 +98,7 @@ def run_case(cuda, side, layout, fmt, opS, opA, dtype, alpha, beta, dims, offs, 
         S = rb.DenseSkOp(rb.DenseDist(SR, SC), rb.RNGState(3), buff=dev(Sfull.ravel(order="F"), cuda), buff_layout="C")
     else:
         Sfull = O.fill_dense("R", SR, SC, "G", "L", SR, SC, 0, 0, key=3, dtype=dtype)[0].reshape(SR, SC)
-        S = rb.DenseSkOp(rb.DenseDist(SR, SC), rb.RNGState(3))
+        S = rb.DenseSkOp(rb.DenseDist(SR, SC), rb.RNGState(3, rng=rng))
     Ssub = Sfull[ro_s:ro_s + ssR, co_s:co_s + ssC].astype(np.float64)
     Asub = Adense[ro_a:ro_a + saR, co_a:co_a + saC].astype(np.float64)
     ldb = (bR if layout == "C" else bC) + 2

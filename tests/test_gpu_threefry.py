@@ -14,6 +14,7 @@ import torch
 import oracle_lib as O
 import randblas_amd as rb
 import test_gpu_dense as TD
+import test_gpu_sksp as TSP
 import test_gpu_sksy as TSY
 import test_gpu_sparse as TS
 
@@ -185,3 +186,15 @@ def test_lskges_threefry_submatrix_transposed(cuda, threefry, opS):
     d, m, n = 15, 180, 9
     SR, SC = (d + 4, m + 21) if opS == "N" else (m + 4, d + 21)
     TS.check_left(cuda, "C", opS, "N", d, n, m, 1.0, 0.0, SR, SC, 3, "S", 0, 2, 5, np.float64, rng="threefry")
+
+
+@pytest.mark.parametrize("side", ["left", "right"])
+@pytest.mark.parametrize("layout", ["C", "R"])
+@pytest.mark.parametrize("fmt", TSP.FMTS)
+@pytest.mark.parametrize("opS", ["N", "T"])
+def test_sketch_sparse_threefry(cuda, threefry, side, layout, fmt, opS):
+    """sketch_sparse (sksp.hh:147-194, 302-345) with a Threefry operator: its window filled on the
+    device by Threefry, then the sparse apply; within E of the oracle's Threefry operator."""
+    dims = (30, 40, 200) if side == "left" else (40, 30, 200)
+    TSP.run_case(cuda, side, layout, fmt, opS, "N", np.float64, 1.5, -0.5, dims, (1, 2, 1, 3), rng="threefry")
+
