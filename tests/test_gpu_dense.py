@@ -154,6 +154,19 @@ def test_lskge3_explicit_buffer(cuda, layout, opS, dtype):
     check_left(cuda, layout, opS, "N", d, n, m, 1.0, 0.5, SR, SC, 1, 2, dtype, explicit=True)
 
 
+@pytest.mark.parametrize("layout", ["C", "R"])
+@pytest.mark.parametrize("opS", ["N", "T"])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("shape", [(300, 40, 256), (512, 64, 1024)])
+def test_lskge3_explicit_buffer_lifting(cuda, layout, opS, dtype, shape):
+    """An explicit S.buff with more output rows than columns (d > n): the data matrix, the operand with
+    fewer outer indices, takes the streamed kernel's loaded side (FAM_MAT) and S streams as the
+    memory operand. Within E of the oracle."""
+    d, n, m = shape
+    SR, SC = (d, m) if opS == "N" else (m, d)
+    check_left(cuda, layout, opS, "N", d, n, m, 1.0, -0.5, SR, SC, 0, 0, dtype, explicit=True)
+
+
 def test_lskge3_alpha_zero_beta(cuda):
     d, n, m = 20, 30, 40
     B0 = np.random.default_rng(0).standard_normal(d * n)
