@@ -2360,9 +2360,10 @@ static bool mat_problem(const GemmProblem &p, GemmProblem &q, int &gk, bool &gx,
 // address: the plan looks at alignment only); whether it takes that route
 // A Philox window the drawing kernels cannot take (a window that does not start on a Philox quad
 // along the counter, K off the step depth with f64, ...: the generic kernel, 4-66 % of the f64 peak)
-// is drawn first as well when the call is large enough (GEN_FIRST_FLOPS) and the window then streams:
-// the reference's own fill_dense + gemm, with the streamed kernel.
-constexpr double GEN_FIRST_FLOPS = 1e9;
+// is drawn first as well when the window is large enough (GEN_FIRST_ENTRIES) and then streams: the
+// reference's own fill_dense + gemm, with the streamed kernel. (A window size, not a flop count, so
+// that column chunks of one call -- randblas_amd.distributed -- take the route the whole call takes.)
+constexpr double GEN_FIRST_ENTRIES = 1 << 20;
 template <typename T> static bool stream_t_ok(const GemmProblem &p);
 template <typename T> static bool wide32_ok(const GemmProblem &p);
 static bool fused_ok(const GemmProblem &p);
@@ -2377,7 +2378,7 @@ static bool drawn_first(const GemmProblem &p, GemmProblem &q) {
     d.materialise = 0;
     const bool generic = !threefry_gen(p) && !stream_ok<T>(d) && !stream_t_ok<T>(d) && !wide_ok<T>(d) &&
                          !wide32_ok<T>(d) && !fused_ok(d) &&
-                         2.0 * (double)p.M * (double)p.N * (double)p.K >= GEN_FIRST_FLOPS;
+                         (double)(p.xkind != MEM ? p.M : p.N) * (double)p.K >= GEN_FIRST_ENTRIES;
     if (!(threefry_gen(p) || p.materialise || generic)) return false;
     q = p;
     for (int side = 0; side < 2; ++side)
