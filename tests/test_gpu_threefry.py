@@ -198,3 +198,22 @@ def test_sketch_sparse_threefry(cuda, threefry, side, layout, fmt, opS):
     dims = (30, 40, 200) if side == "left" else (40, 30, 200)
     TSP.run_case(cuda, side, layout, fmt, opS, "N", np.float64, 1.5, -0.5, dims, (1, 2, 1, 3), rng="threefry")
 
+
+
+@pytest.mark.parametrize("dims", [(0, 5, 7), (4, 0, 7), (4, 5, 0)])
+@pytest.mark.parametrize("explicit", [False, True])
+def test_threefry_and_explicit_degenerate_sizes(cuda, threefry, dims, explicit):
+    """Empty output or empty contraction (the reference's early returns / beta scaling: skge.hh:197-206):
+    B = beta B for m = 0, nothing touched for d = 0 or n = 0."""
+    d, n, m = dims
+    SR, SC = max(d, 1), max(m, 1)
+    S = rb.DenseSkOp(rb.DenseDist(SR, SC), rb.RNGState(2, rng="threefry"))
+    if explicit:
+        S.buff, S.buff_layout = torch.zeros(SR * SC, dtype=torch.float64, device=cuda), "C"
+    A = torch.ones(max(m * n, 1), dtype=torch.float64, device=cuda)
+    B0 = np.arange(1, max(d * n, 1) + 1, dtype=np.float64)
+    dB = TD.dev(B0, cuda)
+    rb.sketch_general_left("C", "N", "N", d, n, m, 1.0, S, A, max(m, 1), 0.5, dB, max(d, 1))
+    got = TD.host(dB)
+    exp = B0 * 0.5 if (m == 0 and d > 0 and n > 0) else B0
+    assert np.array_equal(got, exp)
