@@ -219,6 +219,22 @@ int rbh_rskge3_plan_f64(char layout, char opA, char opS, int64_t m, int64_t d, i
 int rbh_rskge3_plan_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, const float *A, int64_t lda,
                         const rbh_dense_dist *D, const float *S_buff, char S_layout, int64_t ro_s, int64_t co_s,
                         int64_t ldb, const rbh_options *opt, rbh_plan *plan);
+/* The same with the operator's state (ABI 4): the plan of a Threefry operator is that of its window
+ * drawn into a workspace first (the GEMM kernels draw Philox only); seed NULL = a Philox operator. */
+int rbh_lskge3_plan_st_f64(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, const rbh_dense_dist *D,
+                           const rbh_state *seed, const double *S_buff, char S_layout, int64_t ro_s, int64_t co_s,
+                           const double *A, int64_t lda, int64_t ldb, const rbh_options *opt, rbh_plan *plan);
+int rbh_lskge3_plan_st_f32(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, const rbh_dense_dist *D,
+                           const rbh_state *seed, const float *S_buff, char S_layout, int64_t ro_s, int64_t co_s,
+                           const float *A, int64_t lda, int64_t ldb, const rbh_options *opt, rbh_plan *plan);
+int rbh_rskge3_plan_st_f64(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, const double *A,
+                           int64_t lda, const rbh_dense_dist *D, const rbh_state *seed, const double *S_buff,
+                           char S_layout, int64_t ro_s, int64_t co_s, int64_t ldb, const rbh_options *opt,
+                           rbh_plan *plan);
+int rbh_rskge3_plan_st_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, const float *A,
+                           int64_t lda, const rbh_dense_dist *D, const rbh_state *seed, const float *S_buff,
+                           char S_layout, int64_t ro_s, int64_t co_s, int64_t ldb, const rbh_options *opt,
+                           rbh_plan *plan);
 
 /* The sparse sketches with per-call options (sparse_filled above). */
 int rbh_lskges_ex_f64(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, double alpha,

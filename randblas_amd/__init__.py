@@ -127,6 +127,12 @@ for _t, _ct in (("f64", ctypes.c_double), ("f32", ctypes.c_float)):
     getattr(lib, f"rbh_rskge3_plan_{_t}").argtypes = [c_char, c_char, c_char, c_i64, c_i64, c_i64, c_vp, c_i64,
                                                       P(DenseDistC), c_vp, c_char, c_i64, c_i64, c_i64, P(OptionsC),
                                                       P(PlanC)]
+    getattr(lib, f"rbh_lskge3_plan_st_{_t}").argtypes = [c_char, c_char, c_char, c_i64, c_i64, c_i64, P(DenseDistC),
+                                                         P(RNGStateC), c_vp, c_char, c_i64, c_i64, c_vp, c_i64, c_i64,
+                                                         P(OptionsC), P(PlanC)]
+    getattr(lib, f"rbh_rskge3_plan_st_{_t}").argtypes = [c_char, c_char, c_char, c_i64, c_i64, c_i64, c_vp, c_i64,
+                                                         P(DenseDistC), P(RNGStateC), c_vp, c_char, c_i64, c_i64, c_i64,
+                                                         P(OptionsC), P(PlanC)]
 lib.rbh_is_device_pointer.argtypes = [c_vp]
 lib.rbh_release_workspaces.argtypes = [c_vp]
 lib.rbh_release_workspaces_ex.argtypes = [c_vp, ctypes.c_int]
@@ -484,24 +490,26 @@ def _plan(c: PlanC) -> Plan:
 
 def plan_left(layout, opS, opA, d, n, m, S: DenseSkOp, A, lda, ldb, ro_s=0, co_s=0, dtype="f64",
               options: Optional[Options] = None) -> Plan:
-    """The kernel, split-K factor and tiles sketch_general_left would use (rbh_lskge3_plan); A is only
-    inspected for its alignment (a device tensor, a host array, or an integer address)."""
+    """The kernel, split-K factor and tiles sketch_general_left would use (rbh_lskge3_plan_st: the
+    operator's generator included); A is only inspected for its alignment (a device tensor, a host
+    array, or an integer address)."""
     out = PlanC()
     a = A if isinstance(A, int) else _ptr(A)
-    _check(getattr(lib, f"rbh_lskge3_plan_{dtype}")(_b(layout), _b(opS), _b(opA), d, n, m, ctypes.byref(S.dist.c()),
-                                                     _ptr(S.buff), _b(S.buff_layout), ro_s, co_s, a, lda, ldb,
-                                                     _opt(options), ctypes.byref(out)))
+    _check(getattr(lib, f"rbh_lskge3_plan_st_{dtype}")(_b(layout), _b(opS), _b(opA), d, n, m, ctypes.byref(S.dist.c()),
+                                                        ctypes.byref(S.seed_state.c()), _ptr(S.buff), _b(S.buff_layout),
+                                                        ro_s, co_s, a, lda, ldb, _opt(options), ctypes.byref(out)))
     return _plan(out)
 
 
 def plan_right(layout, opA, opS, m, d, n, A, lda, S: DenseSkOp, ldb, ro_s=0, co_s=0, dtype="f64",
                options: Optional[Options] = None) -> Plan:
-    """The plan of sketch_general_right (rbh_rskge3_plan)."""
+    """The plan of sketch_general_right (rbh_rskge3_plan_st)."""
     out = PlanC()
     a = A if isinstance(A, int) else _ptr(A)
-    _check(getattr(lib, f"rbh_rskge3_plan_{dtype}")(_b(layout), _b(opA), _b(opS), m, d, n, a, lda,
-                                                     ctypes.byref(S.dist.c()), _ptr(S.buff), _b(S.buff_layout), ro_s,
-                                                     co_s, ldb, _opt(options), ctypes.byref(out)))
+    _check(getattr(lib, f"rbh_rskge3_plan_st_{dtype}")(_b(layout), _b(opA), _b(opS), m, d, n, a, lda,
+                                                        ctypes.byref(S.dist.c()), ctypes.byref(S.seed_state.c()),
+                                                        _ptr(S.buff), _b(S.buff_layout), ro_s, co_s, ldb,
+                                                        _opt(options), ctypes.byref(out)))
     return _plan(out)
 
 

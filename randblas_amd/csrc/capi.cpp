@@ -1423,19 +1423,21 @@ int sketch_symmetric(char layout, char side, int64_t d, int64_t n, T alpha, cons
 template <typename T>
 int dense_plan(bool left, char layout, char opS, char opA, int64_t M1, int64_t M2, int64_t M3, const rbh_dense_dist *D,
                const T *S_buff, char S_layout, int64_t ro_s, int64_t co_s, const T *A, int64_t lda, int64_t ldb,
-               const rbh_options *opt, rbh_plan *plan) {
+               const rbh_options *opt, rbh_plan *plan, const rbh_state *seed = nullptr) {
     int rc = check_options(opt);
     if (rc) return rc;
     RBH_REQUIRE(plan != nullptr && D != nullptr);
+    if (seed) RBH_REQUIRE(seed->rng == RBH_RNG_PHILOX4X32 || seed->rng == RBH_RNG_THREEFRY4X32);
     RBH_REQUIRE(layout == 'C' || layout == 'R');
     RBH_REQUIRE(opS == 'N' || opS == 'T');
     RBH_REQUIRE(opA == 'N' || opA == 'T');
     RBH_REQUIRE(M1 >= 0 && M2 >= 0 && M3 >= 0 && ro_s >= 0 && co_s >= 0);
     static const rbh_state zero{};
+    const rbh_state *st = seed ? seed : &zero;   // (the plan depends on the generator, not on the counter/key)
     GemmProblem p{};
-    if (left) build_left<T>(p, layout, opS, opA, M1, M2, M3, (T)1, (T)0, D, &zero, S_buff, S_layout, ro_s, co_s, A, lda,
+    if (left) build_left<T>(p, layout, opS, opA, M1, M2, M3, (T)1, (T)0, D, st, S_buff, S_layout, ro_s, co_s, A, lda,
                             nullptr, ldb);
-    else build_right<T>(p, layout, opA, opS, M1, M2, M3, (T)1, (T)0, A, lda, D, &zero, S_buff, S_layout, ro_s, co_s,
+    else build_right<T>(p, layout, opA, opS, M1, M2, M3, (T)1, (T)0, A, lda, D, st, S_buff, S_layout, ro_s, co_s,
                         nullptr, ldb);
     apply_options(p, opt);
     const GemmPlan g = sizeof(T) == 8 ? plan_gemm_f64(p) : plan_gemm_f32(p);
@@ -1798,6 +1800,32 @@ int rbh_rskge3_plan_f32(char layout, char opA, char opS, int64_t m, int64_t d, i
                         const rbh_dense_dist *D, const float *S_buff, char S_layout, int64_t ro_s, int64_t co_s,
                         int64_t ldb, const rbh_options *opt, rbh_plan *plan) {
     return dense_plan<float>(false, layout, opS, opA, m, d, n, D, S_buff, S_layout, ro_s, co_s, A, lda, ldb, opt, plan);
+}
+int rbh_lskge3_plan_st_f64(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, const rbh_dense_dist *D,
+                           const rbh_state *seed, const double *S_buff, char S_layout, int64_t ro_s, int64_t co_s,
+                           const double *A, int64_t lda, int64_t ldb, const rbh_options *opt, rbh_plan *plan) {
+    return dense_plan<double>(true, layout, opS, opA, d, n, m, D, S_buff, S_layout, ro_s, co_s, A, lda, ldb, opt, plan,
+                              seed);
+}
+int rbh_lskge3_plan_st_f32(char layout, char opS, char opA, int64_t d, int64_t n, int64_t m, const rbh_dense_dist *D,
+                           const rbh_state *seed, const float *S_buff, char S_layout, int64_t ro_s, int64_t co_s,
+                           const float *A, int64_t lda, int64_t ldb, const rbh_options *opt, rbh_plan *plan) {
+    return dense_plan<float>(true, layout, opS, opA, d, n, m, D, S_buff, S_layout, ro_s, co_s, A, lda, ldb, opt, plan,
+                             seed);
+}
+int rbh_rskge3_plan_st_f64(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, const double *A,
+                           int64_t lda, const rbh_dense_dist *D, const rbh_state *seed, const double *S_buff,
+                           char S_layout, int64_t ro_s, int64_t co_s, int64_t ldb, const rbh_options *opt,
+                           rbh_plan *plan) {
+    return dense_plan<double>(false, layout, opS, opA, m, d, n, D, S_buff, S_layout, ro_s, co_s, A, lda, ldb, opt, plan,
+                              seed);
+}
+int rbh_rskge3_plan_st_f32(char layout, char opA, char opS, int64_t m, int64_t d, int64_t n, const float *A,
+                           int64_t lda, const rbh_dense_dist *D, const rbh_state *seed, const float *S_buff,
+                           char S_layout, int64_t ro_s, int64_t co_s, int64_t ldb, const rbh_options *opt,
+                           rbh_plan *plan) {
+    return dense_plan<float>(false, layout, opS, opA, m, d, n, D, S_buff, S_layout, ro_s, co_s, A, lda, ldb, opt, plan,
+                             seed);
 }
 
 }  // extern "C"

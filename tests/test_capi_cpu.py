@@ -257,3 +257,15 @@ def test_unknown_generator_tag_is_refused():
     rc = rb.lib.rbh_dense_next_state(ctypes.byref(rb.DenseDist(30, 200).c()), ctypes.byref(s), ctypes.byref(out))
     assert rc != 0
     assert "seed->rng" in rb.lib.rbh_last_error().decode()
+
+
+def test_plan_follows_the_generator():
+    """rbh_lskge3_plan_st: a Threefry operator's window is drawn first (the GEMM kernels draw Philox
+    only), so a call the fused kernel takes for Philox reads it from memory: the streamed kernel where
+    the window then streams (K a multiple of the step depth), else the generic kernel."""
+    shapes = [((1024, 4096, 16384), "stream", "stream"), ((20, 30, 40), "fused", "generic"),
+              ((100, 3000, 4004), "fused", "generic")]
+    for (d, n, m), philox, threefry in shapes:
+        for rng, want in (("philox", philox), ("threefry", threefry)):
+            S = rb.DenseSkOp(rb.DenseDist(d, m), rb.RNGState(0, rng=rng))
+            assert rb.plan_left("C", "N", "N", d, n, m, S, 256, m, d).kernel == want, (d, n, m, rng)
