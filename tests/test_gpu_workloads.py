@@ -209,3 +209,31 @@ def test_c3_saso_slices_bitwise(cuda):
         assert np.array_equal(got.view(np.uint64), Bexp.view(np.uint64)), f"cols {j0}: {np.sum(got != Bexp)} differ"
     assert bool(torch.isfinite(B).all())
     del A
+
+
+@pytest.mark.parametrize("shape", [("C2", 1024, 16384, 16384), ("NS", 2048, 16384, 16384), ("C1", 128, 4096, 4096)])
+def test_explicit_operator_at_workload_size_bitwise(cuda, shape):
+    """The operator filled once (fill_dense(S), the reference's explicit-buffer usage) and applied from
+    memory (FAM_MAT): the whole output bitwise the fused sketch's, and, with the materialise option,
+    the same again."""
+    _, d, m, n = shape
+    A = device_A(cuda, m, n, torch.float64)
+    S = rb.DenseSkOp(rb.DenseDist(d, m), rb.RNGState(0))
+    out = []
+    for mode in ("fused", "explicit", "materialise"):
+        B = torch.empty(d * n, dtype=torch.float64, device=cuda)
+        op, opts = S, None
+        if mode == "explicit":
+            buf = torch.empty(d * m, dtype=torch.float64, device=cuda)
+            rb.fill_dense("R", rb.DenseDist(d, m), d, m, 0, 0, buf, rb.RNGState(0))
+            op = rb.DenseSkOp(rb.DenseDist(d, m), rb.RNGState(0))
+            op.buff, op.buff_layout = buf, "R"
+        if mode == "materialise":
+            opts = rb.Options(materialise=True)
+        rb.sketch_general_left("C", "N", "N", d, n, m, 1.0, op, A, m, 0.0, B, d, options=opts)
+        torch.cuda.synchronize()
+        out.append(B)
+        if mode == "explicit":
+            del buf
+    assert torch.equal(out[0].view(torch.int64), out[1].view(torch.int64))
+    assert torch.equal(out[0].view(torch.int64), out[2].view(torch.int64))
