@@ -10,7 +10,9 @@
 // ---- skge_dense.hip: the streamed GEMM (skge_stream_kernel) ---------------------------------
 // memory-operand prefetch depth, in part-blocks ahead of their use: f64 7 (64 x 512 tiles: C2 7.97-7.98
 // ms against 7.99-8.02 with 3; 32 x 1024 tiles: C2 7.66-7.68 against 7.70-7.71 with 3, C5 3.91 against
-// 4.02-4.08), f32 3 (C4 4.08-4.11 against 4.18-4.20 with 1), the one-triangle forms 7
+// 4.02-4.08; with rounds of 8, NS 15.27-15.30 against 15.43-15.46 with 3), f32 3 (C4 4.08-4.11 against
+// 4.18-4.20 with 1), the one-triangle forms 3 since the rounds of 8 (C5p kernel 4.084-4.089 ms against
+// 4.158-4.177 with 7 and 4.36-4.38 with 1; profiles/r06/ab_pf_tri.jsonl)
 #ifndef RBH_PF64
 #define RBH_PF64 7
 #endif
@@ -18,11 +20,11 @@
 #define RBH_PF32 3
 #endif
 #ifndef RBH_PF_TRI
-#define RBH_PF_TRI 7
+#define RBH_PF_TRI 3
 #endif
 // prefetch depth of the 32-row transposed-operand forms (TRI 5; their part-blocks are four 8-B
 // loads): f64 32 x 1024 PF 7 7.74-7.77 ms against 7.80-7.82 with 3 at d = 1024, m = n = 16384, same
-// box, two alternations
+// box, two alternations (with rounds of 8: 7.64-7.67 against 7.72-7.75, profiles/r06/ab_pf_stream.jsonl)
 #ifndef RBH_PF_TRI32
 #define RBH_PF_TRI32 7
 #endif
